@@ -1,0 +1,215 @@
+"""CPU ORACLE (test infrastructure only).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module, and only as the checker.  It wraps:
+
+* ``_build/liboracle.so`` — gh_oracle.c, a bit-serial C restatement of the
+  reference encoder/decoder semantics (file:line citations in gh_oracle.c);
+* ``_ref/*`` — the reference's own CPU programs/functions compiled from its
+  sources by oracle/Makefile (sequential.cpp, parallel_cpu_decomp.cpp,
+  parallel_cpu_prescan.cpp, boundary_PM via ref_drivers/pm_driver.cpp,
+  get_twolevel_table via ref_drivers/table_probe.cpp).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import shutil
+import subprocess
+import tempfile
+import time
+from typing import Optional
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "_build", "liboracle.so")
+REF = os.path.join(HERE, "_ref")
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            raise RuntimeError(f"{LIB} missing: run `make -C {HERE} oracle`")
+        L = ctypes.CDLL(LIB)
+        P, U64, I = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
+        L.orc_package_merge.argtypes = [P, I, P]
+        L.orc_package_merge.restype = I
+        L.orc_plan_make.argtypes = [P, U64, I, P]
+        L.orc_plan_make.restype = I
+        L.orc_encode.argtypes = [P, P, P]
+        L.orc_encode.restype = I
+        L.orc_decode.argtypes = [P, U64, P, U64, ctypes.POINTER(U64)]
+        L.orc_decode.restype = ctypes.c_int64
+        L.orc_segment_count.argtypes = [P, U64, U64]
+        L.orc_segment_count.restype = ctypes.c_int64
+        L.orc_generate.argtypes = [U64, ctypes.c_double, U64, U64, P]
+        L.orc_generate.restype = None
+        _lib = L
+    return _lib
+
+
+class _Plan(ctypes.Structure):
+    _fields_ = [
+        ("n", ctypes.c_uint64), ("bits", ctypes.c_uint64), ("w", ctypes.c_uint64),
+        ("g", ctypes.c_uint64), ("file_bytes", ctypes.c_uint64), ("nsyms", ctypes.c_int),
+        ("version", ctypes.c_int), ("syms", ctypes.c_uint8 * 256), ("lens", ctypes.c_uint8 * 256),
+        ("count", ctypes.c_uint64 * 256),
+    ]
+
+
+def _u8(a) -> np.ndarray:
+    if isinstance(a, (bytes, bytearray, memoryview)):
+        return np.frombuffer(a, dtype=np.uint8)
+    return np.ascontiguousarray(a, dtype=np.uint8)
+
+
+def _p(a: np.ndarray):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def package_merge(sorted_counts) -> list:
+    c = np.ascontiguousarray(sorted_counts, dtype=np.uint64)
+    out = np.zeros(max(1, c.size), dtype=np.uint8)
+    if lib().orc_package_merge(_p(c), c.size, _p(out)) != 0:
+        raise RuntimeError("oracle package-merge failed")
+    return out[: c.size].tolist()
+
+
+def encode(data, force_v2: bool = False) -> np.ndarray:
+    d = _u8(data)
+    plan = _Plan()
+    if lib().orc_plan_make(_p(d), d.size, int(force_v2), ctypes.byref(plan)) != 0:
+        raise RuntimeError("oracle plan failed")
+    out = np.zeros(plan.file_bytes, dtype=np.uint8)
+    if lib().orc_encode(_p(d), ctypes.byref(plan), _p(out)) != 0:
+        raise RuntimeError("oracle encode failed")
+    return out
+
+
+def symbols_of(data) -> list:
+    """File-order (symbol, length) list the reference encoder would write."""
+    d = _u8(data)
+    plan = _Plan()
+    if lib().orc_plan_make(_p(d), d.size, 0, ctypes.byref(plan)) != 0:
+        raise RuntimeError("oracle plan failed")
+    return [(plan.syms[i], plan.lens[i]) for i in range(plan.nsyms)]
+
+
+def decode(file_bytes, out_cap: Optional[int] = None):
+    """Returns (decoded bytes clamped at N, total symbols counted over all segments)."""
+    f = _u8(file_bytes)
+    cap = out_cap if out_cap is not None else max(1, f.size * 8)
+    out = np.zeros(max(1, cap), dtype=np.uint8)
+    total = ctypes.c_uint64()
+    n = lib().orc_decode(_p(f), f.size, _p(out), out.size, ctypes.byref(total))
+    if n < 0:
+        raise RuntimeError("oracle decode failed (bad stream)")
+    return out[:n].copy(), int(total.value)
+
+
+def segment_count(file_bytes, i: int) -> int:
+    f = _u8(file_bytes)
+    r = lib().orc_segment_count(_p(f), f.size, i)
+    if r < 0:
+        raise RuntimeError("oracle segment_count failed")
+    return int(r)
+
+
+def generate(seed: int, redundancy: float, n: int, offset: int = 0) -> np.ndarray:
+    out = np.empty(n, dtype=np.uint8)
+    lib().orc_generate(seed, float(redundancy), offset, n, _p(out))
+    return out
+
+
+# ------------------------------------------------------------------ reference binaries
+def ref_available(name: str) -> bool:
+    return os.access(os.path.join(REF, name), os.X_OK)
+
+
+def ref_package_merge(counts256) -> list:
+    """Reference boundary_PM via _ref/pm_driver: file-order [(symbol, length)]."""
+    c = np.ascontiguousarray(counts256, dtype="<u4")
+    assert c.size == 256
+    with tempfile.TemporaryDirectory() as td:
+        fn = os.path.join(td, "c.bin")
+        c.tofile(fn)
+        out = subprocess.run([os.path.join(REF, "pm_driver"), fn], capture_output=True, text=True,
+                             check=True).stdout
+    return [tuple(int(x) for x in line.split()) for line in out.strip().splitlines()]
+
+
+def ref_table_probe(symbols):
+    """Reference get_twolevel_table via _ref/table_probe (maxlen > 10 only).
+
+    Returns (l1_size, l2_size, ptr_size, table bytes) or None when unsupported."""
+    with tempfile.TemporaryDirectory() as td:
+        fn = os.path.join(td, "s.txt")
+        with open(fn, "w") as f:
+            for s, l in symbols:
+                f.write(f"{s} {l}\n")
+        r = subprocess.run([os.path.join(REF, "table_probe"), fn], capture_output=True)
+    if r.returncode != 0:
+        return None
+    hdr = np.frombuffer(r.stdout[:16], dtype="<u4")
+    return int(hdr[0]), int(hdr[1]), int(hdr[2]), np.frombuffer(r.stdout[16:16 + int(hdr[3])], dtype=np.uint8)
+
+
+def ref_table_lookup(table_info, window: int, prefix_bit: int = 10):
+    """Replay of the reference kernel lookup (decoder.cu:531-546) on a 32-bit window.
+
+    Returns (symbol, length)."""
+    l1, l2, ptr, tb = table_info
+    ptr_table = tb[: 4 * ptr].view("<u4") if ptr else np.zeros(0, dtype="<u4")
+    length_table = tb[4 * ptr: 4 * ptr + 256]
+    l1_table = tb[4 * ptr + 256: 4 * ptr + 256 + l1]
+    l2_table = tb[4 * ptr + 256 + l1: 4 * ptr + 256 + l1 + l2]
+    prefix_mask = (~((0xFFFFFFFF) >> prefix_bit)) & 0xFFFFFFFF
+    deccode = (window & prefix_mask) >> (32 - prefix_bit)
+    if deccode < l1:
+        sym = int(l1_table[deccode])
+    else:
+        t = int(ptr_table[deccode - l1])
+        width = (t >> 16) & 0xFFFF
+        idx = t & 0xFFFF
+        l2_mask = ((~(0xFFFFFFFF >> width)) & 0xFFFFFFFF) >> prefix_bit
+        l2_shift = 32 - prefix_bit - width
+        sym = int(l2_table[idx + ((window & l2_mask) >> l2_shift)])
+    return sym, int(length_table[sym])
+
+
+_SEQ_RE = re.compile(r"Decompression time:\s+(\d+) mcs")
+_PAR_RE = re.compile(r"Decompression time \(Parallel Decode\):\s+(\d+) us")
+_VER_RE = re.compile(r"Verification:\s+(PASS|FAIL)")
+
+
+def run_reference_cpu(name: str, data: np.ndarray, timeout: float = 600.0) -> dict:
+    """Run a reference CPU program (compiled from its own source) on `data`.
+
+    sequential / parallel_cpu_prescan read data100_100.bin, parallel_decomp_cpu
+    reads data.bin (sequential.cpp:240, parallel_cpu_prescan.cpp:596,
+    parallel_cpu_decomp.cpp:655); each times decode() only and verifies.
+    Returns {decode_us, verified, threads, wall_s}."""
+    exe = os.path.join(REF, name)
+    if not os.access(exe, os.X_OK):
+        raise FileNotFoundError(exe)
+    infile = "data.bin" if name == "parallel_decomp_cpu" else "data100_100.bin"
+    td = tempfile.mkdtemp(prefix="gh_ref_")
+    try:
+        _u8(data).tofile(os.path.join(td, infile))
+        t0 = time.time()
+        r = subprocess.run([exe], cwd=td, capture_output=True, text=True, timeout=timeout)
+        wall = time.time() - t0
+        m = (_SEQ_RE if name == "sequential" else _PAR_RE).search(r.stdout)
+        v = _VER_RE.search(r.stdout)
+        if not m:
+            raise RuntimeError(f"{name} produced no timing: {r.stdout[-400:]} {r.stderr[-400:]}")
+        threads = {"sequential": 1, "parallel_decomp_cpu": 1, "parallel_cpu_prescan": 16}[name]
+        return {"decode_us": int(m.group(1)), "verified": bool(v and v.group(1) == "PASS"),
+                "threads": threads, "wall_s": wall}
+    finally:
+        shutil.rmtree(td, ignore_errors=True)

@@ -1,0 +1,153 @@
+"""GPU parity tests: the HIP decoder (through the C ABI) against the CPU oracle and
+the original input, bit-exact.  Reference semantics: Huffman_coding_Gap_arrays/
+decoder/src/decoder.cu:454-730 (see oracle/gh_oracle.c for the restatement)."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _roundtrip(gh, orc, data, **kw):
+    img = gh.encode(data)
+    out = gh.decode(img, **kw)
+    ref, _ = orc.decode(img)
+    assert ref.size == len(data) and np.array_equal(ref, np.asarray(data, dtype=np.uint8))
+    assert out.size == len(data)
+    if not np.array_equal(out, ref):
+        bad = np.nonzero(out != ref)[0]
+        raise AssertionError(f"{bad.size} mismatches, first at {bad[0]} of {out.size}")
+    return img
+
+
+@pytest.mark.parametrize("r", [0.0, 0.1, 0.5, 0.9, 0.999, 1.0])
+@pytest.mark.parametrize("n", [1, 2, 7, 100, 4097, 65549, 1_000_003])
+def test_generated_vs_oracle(gpu, orc, r, n):
+    data = gpu.generate(1000 + n, r, n)
+    _roundtrip(gpu, orc, data)
+
+
+def test_single_symbol(gpu, orc):
+    for n in (1, 5, 128, 129, 100_000):
+        _roundtrip(gpu, orc, np.full(n, 65, dtype=np.uint8))
+
+
+def test_two_symbols_one_bit_codes(gpu, orc):
+    rng = np.random.default_rng(3)
+    for n in (10, 1000, 300_001):
+        data = rng.integers(0, 2, n).astype(np.uint8) + 48
+        img = _roundtrip(gpu, orc, data)
+        assert max(l for _, l in gpu.parse(img).symbols) == 1
+
+
+def test_long_codes_up_to_16_bits(gpu, orc):
+    # geometric counts force length-limited codes up to MAX_CODEWORD_LENGTH = 16
+    counts = [max(1, int(2 ** (24 - 0.9 * i))) for i in range(40)]
+    data = np.repeat(np.arange(40, dtype=np.uint8), counts)
+    np.random.default_rng(5).shuffle(data)
+    img = _roundtrip(gpu, orc, data)
+    assert max(l for _, l in gpu.parse(img).symbols) == 16
+
+
+def test_exact_segment_multiple(gpu, orc):
+    # 256 equal counts -> all codes 8 bits; n = 16k -> bits is a multiple of 128
+    data = np.tile(np.arange(256, dtype=np.uint8), 64)
+    np.random.default_rng(9).shuffle(data)
+    img = _roundtrip(gpu, orc, data)
+    s = gpu.parse(img)
+    assert s.w * 32 == s.g * 128
+
+
+@pytest.mark.parametrize("k", [1, 6, 8, 10, 12])
+def test_lut_widths(gpu, orc, k, monkeypatch):
+    monkeypatch.setenv("GH_LUT_BITS", str(k))
+    for r in (0.1, 0.9):
+        _roundtrip(gpu, orc, gpu.generate(77, r, 200_000))
+
+
+@pytest.mark.parametrize("nshards", [2, 3, 8])
+def test_shards_on_one_device(gpu, orc, nshards):
+    data = gpu.generate(11, 0.5, 2_000_000)
+    _roundtrip(gpu, orc, data, ngpus=nshards, devices=[0] * nshards)
+
+
+def test_shard_counts_match_oracle(gpu, orc):
+    data = gpu.generate(12, 0.9, 300_000)
+    img = gpu.encode(data)
+    s = gpu.parse(img)
+    bounds = gpu.plan_shards(s.g, 5)
+    off = 0
+    for k in range(5):
+        with gpu.Decoder(0) as d:
+            d.load(s, bounds[k], bounds[k + 1])
+            d.decode()
+            r = d.report()
+            expect = sum(orc.segment_count(img, i) for i in range(bounds[k], bounds[k + 1]))
+            assert r.symbols == expect
+            keep = min(r.symbols, s.n - off)
+            got = d.download(keep)
+            assert np.array_equal(got, data[off:off + keep])
+            off += r.symbols
+
+
+def test_repeated_decodes_identical(gpu):
+    data = gpu.generate(13, 0.5, 3_000_000)
+    img = gpu.encode(data)
+    s = gpu.parse(img)
+    with gpu.Decoder(0) as d:
+        d.load(s)
+        for _ in range(5):
+            d.decode()
+        r = d.report()
+        assert r.launches == 5 and r.status == 0 and r.symbols >= s.n
+        assert np.array_equal(d.download(s.n), data)
+
+
+def test_reference_launcher_mirror(gpu):
+    data = gpu.generate(14, 0.9, 123_457)
+    img = gpu.encode(data)
+    s = gpu.parse(img)
+    words = np.concatenate([np.frombuffer(s.raw[len(s.raw) - 4 * (s.w + (s.g + 7) // 8):].tobytes(),
+                                          dtype=np.uint32)])
+    out = gpu.decoder_l1_l2(words, s.w, s.n, s.g, s.symbols)
+    assert np.array_equal(out, data)
+
+
+def test_corrupted_stream_terminates(gpu):
+    data = gpu.generate(15, 0.9, 500_000)
+    img = gpu.encode(data).copy()
+    rng = np.random.default_rng(1)
+    hdr = 8 + 2 * len(gpu.parse(img).symbols) + 12
+    for pos in rng.integers(hdr, img.size, 200):
+        img[pos] ^= 0xFF
+    try:
+        out = gpu.decode(img)  # either an error or a bounded, wrong output
+        assert out.size == data.size
+    except gpu.GapHuffError as e:
+        assert e.code in (-7, -2)
+
+
+def test_empty_stream(gpu):
+    img = gpu.encode(b"")
+    assert gpu.decode(img).size == 0
+
+
+@pytest.mark.parametrize("cfg", [("cfg2", 10**8, 0.5)])
+def test_config2_100MB_bitexact(gpu, cfg):
+    _, n, r = cfg
+    data = gpu.generate(375, r, n)
+    img = gpu.encode(data)
+    out = gpu.decode(img)
+    assert np.array_equal(out, data)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("cfg", [("cfg3", 10**9, 0.9), ("cfg4", 10**9, 0.1)])
+def test_config_1GB_bitexact(gpu, cfg):
+    # size-independent property at full size: decode(encode(x)) == x
+    _, n, r = cfg
+    data = gpu.generate(375, r, n)
+    img = gpu.encode(data)
+    out = gpu.decode(img)
+    assert np.array_equal(out, data)
