@@ -40,13 +40,13 @@
 
 namespace gh {
 
-constexpr int TB = 256;                  // workgroup size = segments per tile
+constexpr int TB = 256;                  // workgroup size = segments per sub-tile
 constexpr int NWAVE = TB / 64;
-constexpr int SLOT_WORDS = 5;            // 4 segment words + 1 look-ahead word
-constexpr int IN_BYTES = ((4 + 4 * SLOT_WORDS * TB) + 15) & ~15;
 constexpr int FB_WORDS = 3 * 17 + 64;    // limit16/base16/first + 256 symbol bytes
 constexpr int FB_BYTES = ((4 * FB_WORDS) + 15) & ~15;
-constexpr int SCRATCH_BYTES = 64;
+constexpr int MAX_SUPER = 8;             // sub-tiles per super-tile (template values 1,2,4,8)
+constexpr int SCRATCH_BYTES = 4 * (MAX_SUPER * NWAVE + 8);
+constexpr int SLOT_BYTES = 40 * TB;
 constexpr uint32_t EPOCH_MAX = (1u << 24) - 1;
 constexpr uint32_t SPIN_LIMIT = 1u << 22;
 
@@ -56,37 +56,41 @@ struct DecodeParams {
   const uint4* lut;              // 2^K entries as {syms, meta} pairs (8 bytes)
   const uint32_t* fb;            // fallback tables
   uint8_t* out;                  // shard output
-  unsigned long long* granules;  // one per tile
+  unsigned long long* granules;  // one per super-tile
   unsigned int* ticket;
   unsigned int* status;
-  unsigned long long* total;     // shard symbol total (written by the last tile)
+  unsigned long long* total;     // shard symbol total (written by the last super-tile)
   unsigned long long out_cap;
   unsigned long long nseg;
   unsigned int gap_nib0;
   unsigned int first_start;
-  unsigned int ntiles;
+  unsigned int nsuper;           // super-tiles of S*TB segments
   unsigned int kbits;
   unsigned int epoch;
   unsigned int lut_bytes;
   unsigned int stage_bytes;
   unsigned int fb_lo, fb_hi;     // fallback length range
+  unsigned long long* stamps;    // diagnostic build only (GH_STAMPS): per-block phase cycles
 };
+
+// Diagnostic phase stamps (compiled only with -DGH_STAMPS; never in the shipped
+// library): lane 0 of wave 0 accumulates s_memtime deltas per phase.
+#ifdef GH_STAMPS
+#define GH_NSTAMP 10
+#define STAMP_DECL unsigned long long st_acc[GH_NSTAMP] = {}; unsigned long long st_last = __builtin_amdgcn_s_memtime();
+#define STAMP(i) do { if (tid == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); st_acc[i] += t_ - st_last; st_last = t_; } } while (0)
+#define STAMP_FLUSH do { if (tid == 0 && p.stamps) { for (int i_ = 0; i_ < GH_NSTAMP; ++i_) p.stamps[blockIdx.x * 16 + i_] = st_acc[i_]; } } while (0)
+#else
+#define STAMP_DECL
+#define STAMP(i) do {} while (0)
+#define STAMP_FLUSH do {} while (0)
+#endif
 
 // ---- meta word of a LUT entry -------------------------------------------------
 //  [2:0] n symbols (0 = fallback), [7:3] bits consumed, [11:8] e1, [15:12] e2,
 //  [19:16] e3: end of symbol k = start of symbol k+1 (15 when absent).
 __device__ __forceinline__ uint32_t meta_n(uint32_t m) { return m & 7u; }
 __device__ __forceinline__ uint32_t meta_b(uint32_t m) { return (m >> 3) & 31u; }
-
-// 32 stream bits starting at segment-relative bit P (P in [0,128)); slot[-1] must
-// be readable.  alignbit(a,b,s) = ({a,b} >> s)[31:0]; with q = (P-1)>>5 the shift
-// (-P)&31 is in [0,31] for every P, so no shift-by-32 case exists.
-__device__ __forceinline__ uint32_t window32(const uint32_t* slot, int P) {
-  const int q = (P - 1) >> 5;
-  const uint32_t a = slot[q];
-  const uint32_t b = slot[q + 1];
-  return __builtin_amdgcn_alignbit(a, b, (uint32_t)(-P));
-}
 
 // Canonical decode of a codeword longer than the LUT width (rare).  Returns
 // (symbol << 8) | length; a pattern outside the code space sets GH_ST_BADCODE and
@@ -107,18 +111,11 @@ __device__ __noinline__ uint32_t fallback_decode(const uint32_t* fb, uint32_t w1
   return ((uint32_t)syms[0] << 8) | hi;
 }
 
-__device__ __forceinline__ uint32_t fetch_meta(const uint2* lut, const uint32_t* fb, uint32_t t,
-                                               uint32_t kshift, const DecodeParams& p,
-                                               uint32_t* syms) {
-  const uint2 e = lut[t >> kshift];
-  uint32_t meta = e.y;
-  *syms = e.x;
-  if (meta_n(meta) == 0) {
-    const uint32_t r = fallback_decode(fb, t >> 16, p.fb_lo, p.fb_hi, p.status);
-    *syms = r >> 8;
-    meta = 1u | ((r & 31u) << 3) | 0xFFF00u;
-  }
-  return meta;
+__device__ __forceinline__ uint32_t fallback_meta(const uint32_t* fb, uint32_t t,
+                                                  const DecodeParams& p, uint32_t* syms) {
+  const uint32_t r = fallback_decode(fb, t >> 16, p.fb_lo, p.fb_hi, p.status);
+  *syms = r >> 8;
+  return 1u | ((r & 31u) << 3) | 0xFFF00u;
 }
 
 // Symbols of the final lookup that start before the segment end (rem bits left).
@@ -126,6 +123,80 @@ __device__ __forceinline__ uint32_t kept_in_last(uint32_t meta, int rem) {
   const uint32_t r = (uint32_t)min(rem, 15);
   return 1u + (((meta >> 8) & 15u) < r) + (((meta >> 12) & 15u) < r) +
          (((meta >> 16) & 15u) < r);
+}
+
+// Per-thread LDS slot (40 bytes, stride chosen so a wave's ds_read_b64 hits
+// distinct banks): the four overlapping word pairs {w[q], w[q+1]}, q = 0..3.
+// The 32-bit stream window at segment bit P is hi32(pair[P>>5] << (P&31)): one
+// 8-byte LDS read and a 64-bit shift, no shift-by-32 case.
+constexpr int SLOT_U64 = 5;  // 4 pairs + 1 pad (40 B)
+struct Seg {
+  uint32_t w[5];
+  int start;
+};
+
+__device__ __forceinline__ void put_slot(unsigned long long* slot, const Seg& sg) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) slot[q] = ((unsigned long long)sg.w[q] << 32) | sg.w[q + 1];
+}
+
+__device__ __forceinline__ uint32_t window32(const unsigned long long* slot, int P) {
+  return (uint32_t)((slot[P >> 5] << (P & 31)) >> 32);
+}
+
+__device__ __forceinline__ uint32_t count_segment(const unsigned long long* slot, int start,
+                                                  const uint32_t* s_lut32, const uint32_t* fb,
+                                                  uint32_t kshift, const DecodeParams& p) {
+  uint32_t cnt = 0, mlast = 0;
+  int P = start, Plast = start;
+  do {
+    const uint32_t t = window32(slot, P);
+    uint32_t meta = s_lut32[2 * (t >> kshift) + 1];
+    if (meta_n(meta) == 0) {
+      uint32_t sy;
+      meta = fallback_meta(fb, t, p, &sy);
+    }
+    cnt += meta_n(meta);
+    Plast = P;
+    mlast = meta;
+    P += (int)meta_b(meta);
+  } while (P < 128);
+  return cnt - (meta_n(mlast) - kept_in_last(mlast, 128 - Plast));
+}
+
+// Decode the segment again and OR its bytes into the LDS staging buffer starting at
+// byte `bpos`.  A word is flushed only once a later lookup starts, so the final
+// (possibly truncated) lookup's bytes are masked before they reach LDS.
+__device__ __forceinline__ void emit_segment(const unsigned long long* slot, int start,
+                                             const uint2* s_lut, const uint32_t* fb,
+                                             uint32_t kshift, const DecodeParams& p,
+                                             uint32_t* stg, uint32_t bpos) {
+  uint32_t oidx = bpos >> 2;
+  uint32_t fill = 8u * (bpos & 3u);
+  unsigned long long acc = 0;
+  uint32_t mlast = 0;
+  int P = start, Plast = start;
+  do {
+    const uint32_t t = window32(slot, P);
+    const uint2 e = s_lut[t >> kshift];
+    uint32_t meta = e.y, syms = e.x;
+    if (meta_n(meta) == 0) meta = fallback_meta(fb, t, p, &syms);
+    if (fill >= 32) {
+      atomicOr(&stg[oidx], (uint32_t)acc);
+      acc >>= 32;
+      fill -= 32;
+      ++oidx;
+    }
+    acc |= (unsigned long long)syms << fill;
+    fill += 8u * meta_n(meta);
+    Plast = P;
+    mlast = meta;
+    P += (int)meta_b(meta);
+  } while (P < 128);
+  fill -= 8u * (meta_n(mlast) - kept_in_last(mlast, 128 - Plast));
+  acc &= (1ull << fill) - 1ull;  // fill < 64
+  if (fill > 0) atomicOr(&stg[oidx], (uint32_t)acc);
+  if (fill > 32) atomicOr(&stg[oidx + 1], (uint32_t)(acc >> 32));
 }
 
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
@@ -151,14 +222,118 @@ __device__ __forceinline__ unsigned long long granule(unsigned epoch, unsigned f
          (v & ((1ull << 38) - 1));
 }
 
+// Decoupled look-back by one wave: publishes the aggregate, sums predecessors'
+// aggregates back to the nearest inclusive prefix (256 granules per round: lane l
+// reads distances l, l+64, l+128, l+192), publishes the inclusive prefix and
+// returns the exclusive one.  Predecessors hold earlier tickets, so they are
+// running and the spin terminates (bounded anyway by SPIN_LIMIT).
+__device__ unsigned long long look_back(const DecodeParams& p, uint32_t tile,
+                                        unsigned long long total, int lane) {
+  constexpr unsigned long long VMASK = (1ull << 38) - 1;
+  if (tile == 0) {
+    if (lane == 0)
+      __hip_atomic_store(&p.granules[0], granule(p.epoch, 2, total), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    return 0;
+  }
+  if (lane == 0)
+    __hip_atomic_store(&p.granules[tile], granule(p.epoch, 1, total), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  unsigned long long excl = 0;
+  long long base = (long long)tile - 1;
+  uint32_t spins = 0;
+  for (;;) {
+    unsigned long long g[4];
+    uint32_t st[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const long long pi = base - lane - 64 * j;
+      g[j] = 0;
+      st[j] = 2;  // before the first tile: an inclusive 0
+      if (pi >= 0)
+        g[j] = __hip_atomic_load(&p.granules[pi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (base - lane - 64 * j >= 0)
+        st[j] = ((uint32_t)(g[j] >> 40) == p.epoch) ? (uint32_t)((g[j] >> 38) & 3u) : 0u;
+    // nearest inclusive prefix: distance d = 64*j + lane
+    int fp = 256;
+#pragma unroll
+    for (int j = 3; j >= 0; --j) {
+      const unsigned long long pm = __ballot(st[j] == 2);
+      if (pm) fp = 64 * j + __builtin_ctzll(pm);
+    }
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ok &= (64 * j + lane > fp) || (st[j] != 0);
+    if (!__all(ok)) {
+      if (++spins > SPIN_LIMIT) {
+        if (lane == 0) atomicOr(p.status, (unsigned)GH_ST_TIMEOUT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    unsigned long long v = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (64 * j + lane <= fp && base - lane - 64 * j >= 0) v += g[j] & VMASK;
+    excl += wave_sum_u64(v);
+    if (fp < 256) break;
+    base -= 256;
+  }
+  if (lane == 0)
+    __hip_atomic_store(&p.granules[tile], granule(p.epoch, 2, excl + total), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  return excl;
+}
+
+// Copy one sub-tile's staged bytes [lbase, lbase+n) to out[goff, goff+n) clamped at
+// out_cap: 16-byte stores for whole chunks, byte stores for the two edge chunks;
+// zeroes the staging behind itself.
+__device__ __forceinline__ void copy_out(const DecodeParams& p, uint4* st, unsigned long long goff,
+                                         uint32_t n, int tid) {
+  const uint32_t lbase = (uint32_t)(goff & 15);
+  const unsigned long long a0 = goff - lbase;
+  const unsigned long long end = min(goff + n, p.out_cap);
+  const uint32_t nz = (lbase + n + 15u) >> 4;
+  for (uint32_t c = tid; c < nz; c += TB) {
+    const unsigned long long gs = a0 + 16ull * c;
+    const uint4 v = st[c];
+    st[c] = make_uint4(0, 0, 0, 0);
+    if (gs >= goff && gs + 16 <= end) {
+      *(uint4*)(p.out + gs) = v;
+    } else {
+      const uint8_t* b = (const uint8_t*)&v;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const unsigned long long ga = gs + k;
+        if (ga >= goff && ga < end) p.out[ga] = b[k];
+      }
+    }
+  }
+}
+
+// One workgroup processes super-tiles of S*TB segments, drawn from an atomic ticket
+// (the next ticket is prefetched while the current super-tile runs):
+//   1. load the S segments of each thread into registers (16-byte loads);
+//   2. count every segment (LUT-driven walk), scan the S sub-tiles, publish the
+//      super-tile aggregate and run the look-back once;
+//   3. per sub-tile: decode again into LDS staging at the final byte alignment,
+//      then store the sub-tile with 16-byte stores.
+template <int S>
 __global__ __launch_bounds__(TB) void gh_decode_kernel(const DecodeParams p) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint2* s_lut = (uint2*)smem;
+  const uint32_t* s_lut32 = (const uint32_t*)smem;
   uint32_t* s_fb = (uint32_t*)(smem + p.lut_bytes);
-  uint32_t* s_in = (uint32_t*)(smem + p.lut_bytes + FB_BYTES);
-  uint8_t* s_stage = smem + p.lut_bytes + FB_BYTES + IN_BYTES;
+  unsigned long long* s_slots = (unsigned long long*)(smem + p.lut_bytes + FB_BYTES);
+  uint8_t* s_stage = smem + p.lut_bytes + FB_BYTES + SLOT_BYTES;
   uint32_t* s_scr = (uint32_t*)(s_stage + p.stage_bytes);
-  // scratch: [0..3] wave sums, [4] ticket, [6..7] tile offset (u64)
+  // scratch: [0, S*NWAVE) wave sums per sub-tile, [32] ticket, [34..35] super offset
+  uint32_t* s_ticket = s_scr + MAX_SUPER * NWAVE;
+  unsigned long long* s_goff = (unsigned long long*)(s_scr + MAX_SUPER * NWAVE + 2);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -172,177 +347,117 @@ __global__ __launch_bounds__(TB) void gh_decode_kernel(const DecodeParams p) {
     for (uint32_t i = tid; i < (uint32_t)FB_WORDS; i += TB) s_fb[i] = p.fb[i];
     uint4* st = (uint4*)s_stage;
     for (uint32_t i = tid; i < p.stage_bytes / 16; i += TB) st[i] = make_uint4(0, 0, 0, 0);
-    if (tid == 0) s_in[0] = 0;
+    if (tid == 0) *s_ticket = atomicAdd(p.ticket, 1u);
   }
+  __syncthreads();
 
   const uint32_t kshift = 32u - p.kbits;
-  uint32_t* slot = s_in + 1 + SLOT_WORDS * tid;
+  unsigned long long* slot = s_slots + SLOT_U64 * tid;
+  STAMP_DECL
 
   for (;;) {
-    if (tid == 0) s_scr[4] = atomicAdd(p.ticket, 1u);
-    __syncthreads();
-    const uint32_t tile = s_scr[4];
-    if (tile >= p.ntiles) {
-      if (tid == 0 && tile == p.ntiles + gridDim.x - 1)
+    STAMP(9);
+    const uint32_t tile = *s_ticket;
+    if (tile >= p.nsuper) {
+      if (tid == 0 && tile == p.nsuper + gridDim.x - 1)
         __hip_atomic_store(p.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       break;
     }
-    const unsigned long long seg = (unsigned long long)tile * TB + tid;
-    const bool active = seg < p.nseg;
+    uint32_t next = 0;
+    if (tid == 0) next = atomicAdd(p.ticket, 1u);  // consumed at the end of this tile
 
-    // ---- load the segment (16 B vector load, coalesced over the wave) ----------
-    int start = 0;
-    if (active) {
-      const uint4 w = *(const uint4*)(p.payload + 4 * seg);
-      const uint32_t w4 = p.payload[4 * seg + 4];
-      slot[0] = w.x;
-      slot[1] = w.y;
-      slot[2] = w.z;
-      slot[3] = w.w;
-      slot[4] = w4;
-      if (seg == 0) {
-        start = (int)p.first_start;
-      } else {
-        const unsigned long long nib = (unsigned long long)p.gap_nib0 + seg - 1;
-        start = (int)((p.gaps[nib >> 3] >> (4 * (nib & 7))) & 15u);
-      }
-    }
-
-    // ---- pass 1: count codewords starting inside the segment ------------------
-    uint32_t cnt = 0;
-    if (active) {
-      int P = start, Plast = start;
-      uint32_t mlast = 0;
-      do {
-        uint32_t syms;
-        const uint32_t meta = fetch_meta(s_lut, s_fb, window32(slot, P), kshift, p, &syms);
-        cnt += meta_n(meta);
-        Plast = P;
-        mlast = meta;
-        P += (int)meta_b(meta);
-      } while (P < 128);
-      cnt -= meta_n(mlast) - kept_in_last(mlast, 128 - Plast);
-    }
-
-    // ---- tile scan: wave scan + cross-wave combine ------------------------------
-    const uint32_t incl = wave_incl_scan(cnt, lane);
-    if (lane == 63) s_scr[wid] = incl;
-    __syncthreads();
-    uint32_t wpre = 0, tile_total = 0;
+    // ---- 1. load S segments per thread -------------------------------------------
+    Seg sg[S];
+    bool act[S];
+    const unsigned long long seg0 = (unsigned long long)tile * (S * TB) + tid;
 #pragma unroll
-    for (int w = 0; w < NWAVE; ++w) {
-      const uint32_t v = s_scr[w];
-      wpre += (w < wid) ? v : 0u;
-      tile_total += v;
-    }
-    const uint32_t excl_local = wpre + incl - cnt;
-
-    // ---- decoupled look-back over preceding tiles (wave 0) ----------------------
-    if (wid == 0) {
-      unsigned long long excl_tile = 0;
-      if (tile == 0) {
-        if (lane == 0)
-          __hip_atomic_store(&p.granules[0], granule(p.epoch, 2, tile_total), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        if (lane == 0)
-          __hip_atomic_store(&p.granules[tile], granule(p.epoch, 1, tile_total), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-        long long base = (long long)tile - 1;
-        uint32_t spins = 0;
-        for (;;) {
-          const long long pi = base - lane;
-          unsigned long long g = 0;
-          uint32_t st = 2;  // tiles before the first count as an inclusive 0
-          if (pi >= 0) {
-            g = __hip_atomic_load(&p.granules[pi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            st = ((uint32_t)(g >> 40) == p.epoch) ? (uint32_t)((g >> 38) & 3u) : 0u;
-          }
-          const unsigned long long pm = __ballot(st == 2);
-          const unsigned long long vm = __ballot(st != 0);
-          const int fp = pm ? __builtin_ctzll(pm) : 64;
-          const unsigned long long need = (fp >= 63) ? ~0ull : ((2ull << fp) - 1);
-          if ((vm & need) != need) {
-            if (++spins > SPIN_LIMIT) {
-              if (lane == 0) atomicOr(p.status, (unsigned)GH_ST_TIMEOUT);
-              break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-            continue;
-          }
-          const unsigned long long v =
-              (lane <= fp && pi >= 0) ? (g & ((1ull << 38) - 1)) : 0ull;
-          excl_tile += wave_sum_u64(v);
-          if (fp < 64) break;
-          base -= 64;
-        }
-        if (lane == 0)
-          __hip_atomic_store(&p.granules[tile], granule(p.epoch, 2, excl_tile + tile_total),
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      if (lane == 0) {
-        *(unsigned long long*)(s_scr + 6) = excl_tile;
-        if (tile == p.ntiles - 1) *p.total = excl_tile + tile_total;
-      }
-    }
-    __syncthreads();
-    const unsigned long long goff = *(const unsigned long long*)(s_scr + 6);
-    const uint32_t lbase = (uint32_t)(goff & 15);
-
-    // ---- pass 2: decode again, pack bytes into the LDS staging buffer ----------
-    if (active && cnt > 0) {
-      uint32_t* stg = (uint32_t*)s_stage;
-      const uint32_t bpos = lbase + excl_local;
-      uint32_t oidx = bpos >> 2;
-      uint32_t fill = 8u * (bpos & 3u);
-      unsigned long long acc = 0;
-      int P = start, Plast = start;
-      uint32_t mlast = 0;
-      do {
-        uint32_t syms;
-        const uint32_t meta = fetch_meta(s_lut, s_fb, window32(slot, P), kshift, p, &syms);
-        if (fill >= 32) {  // flush a word completed by earlier (non-final) lookups
-          atomicOr(&stg[oidx], (uint32_t)acc);
-          acc >>= 32;
-          fill -= 32;
-          ++oidx;
-        }
-        acc |= (unsigned long long)syms << fill;
-        fill += 8u * meta_n(meta);
-        Plast = P;
-        mlast = meta;
-        P += (int)meta_b(meta);
-      } while (P < 128);
-      fill -= 8u * (meta_n(mlast) - kept_in_last(mlast, 128 - Plast));
-      acc &= (1ull << fill) - 1ull;  // fill < 64
-      if (fill > 0) atomicOr(&stg[oidx], (uint32_t)acc);
-      if (fill > 32) atomicOr(&stg[oidx + 1], (uint32_t)(acc >> 32));
-    }
-    __syncthreads();
-
-    // ---- copy-out: 16-byte chunks, partial edge chunks byte by byte -------------
-    {
-      const unsigned long long a0 = goff - lbase;
-      const unsigned long long end = min(goff + tile_total, p.out_cap);
-      const uint32_t nz = (lbase + tile_total + 15u) >> 4;
-      uint4* st = (uint4*)s_stage;
-      for (uint32_t c = tid; c < nz; c += TB) {
-        const unsigned long long gs = a0 + 16ull * c;
-        const uint4 v = st[c];
-        st[c] = make_uint4(0, 0, 0, 0);
-        if (gs >= goff && gs + 16 <= end) {
-          *(uint4*)(p.out + gs) = v;
+    for (int s = 0; s < S; ++s) {
+      const unsigned long long seg = seg0 + (unsigned long long)s * TB;
+      act[s] = seg < p.nseg;
+      sg[s].start = 0;
+      if (act[s]) {
+        const uint4 w = *(const uint4*)(p.payload + 4 * seg);
+        sg[s].w[0] = w.x;
+        sg[s].w[1] = w.y;
+        sg[s].w[2] = w.z;
+        sg[s].w[3] = w.w;
+        sg[s].w[4] = p.payload[4 * seg + 4];
+        if (seg == 0) {
+          sg[s].start = (int)p.first_start;
         } else {
-          const uint8_t* b = (const uint8_t*)&v;
-#pragma unroll
-          for (int k = 0; k < 16; ++k) {
-            const unsigned long long ga = gs + k;
-            if (ga >= goff && ga < end) p.out[ga] = b[k];
-          }
+          const unsigned long long nib = (unsigned long long)p.gap_nib0 + seg - 1;
+          sg[s].start = (int)((p.gaps[nib >> 3] >> (4 * (nib & 7))) & 15u);
         }
       }
     }
+    STAMP(0);
+
+    // ---- 2. count, scan, look-back --------------------------------------------------
+    uint32_t cnt[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      cnt[s] = 0;
+      if (act[s]) {
+        put_slot(slot, sg[s]);
+        cnt[s] = count_segment(slot, sg[s].start, s_lut32, s_fb, kshift, p);
+      }
+    }
+    STAMP(1);
+    uint32_t excl[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const uint32_t incl = wave_incl_scan(cnt[s], lane);
+      if (lane == 63) s_scr[s * NWAVE + wid] = incl;
+      excl[s] = incl - cnt[s];
+    }
+    __syncthreads();
+    STAMP(2);
+    unsigned long long super_total = 0;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+#pragma unroll
+      for (int w = 0; w < NWAVE; ++w) {
+        const uint32_t v = s_scr[s * NWAVE + w];
+        excl[s] += (w < wid) ? v : 0u;
+        super_total += v;
+      }
+    }
+    if (wid == 0) {
+      const unsigned long long ex = look_back(p, tile, super_total, lane);
+      if (lane == 0) {
+        *s_goff = ex;
+        if (tile == p.nsuper - 1) *p.total = ex + super_total;
+      }
+    }
+    STAMP(3);
+    __syncthreads();
+    STAMP(4);
+
+    // ---- 3. per sub-tile: decode into staging, store -------------------------------
+    unsigned long long goff = *s_goff;
+    uint32_t* stg = (uint32_t*)s_stage;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      uint32_t sub_total = 0;
+#pragma unroll
+      for (int w = 0; w < NWAVE; ++w) sub_total += s_scr[s * NWAVE + w];
+      if (act[s]) {
+        put_slot(slot, sg[s]);
+        emit_segment(slot, sg[s].start, s_lut, s_fb, kshift, p, stg, (uint32_t)(goff & 15) + excl[s]);
+      }
+      STAMP(5);
+      __syncthreads();
+      STAMP(6);
+      copy_out(p, (uint4*)s_stage, goff, sub_total, tid);
+      goff += sub_total;
+      STAMP(7);
+      __syncthreads();
+      STAMP(8);
+    }
+    if (tid == 0) *s_ticket = next;
+    __syncthreads();
   }
+  STAMP_FLUSH;
 }
 
 // ============================================================================
@@ -445,6 +560,15 @@ using namespace gh;
       return fail(GH_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));   \
   } while (0)
 
+static const void* kernel_for(int sv) {
+  switch (sv) {
+    case 8: return (const void*)gh_decode_kernel<8>;
+    case 4: return (const void*)gh_decode_kernel<4>;
+    case 2: return (const void*)gh_decode_kernel<2>;
+    default: return (const void*)gh_decode_kernel<1>;
+  }
+}
+
 struct gh_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -461,8 +585,10 @@ struct gh_ctx {
   unsigned int* d_misc = nullptr;  // [0] ticket, [1] status, [2..3] total
   uint2* d_lut = nullptr;
   uint32_t* d_fb = nullptr;
+  unsigned long long* d_stamps = nullptr;  // GH_STAMPS builds only
   uint32_t epoch = 0;
-  uint32_t ntiles = 0;
+  uint32_t ntiles = 0;   // super-tiles
+  uint32_t super = 1;    // sub-tiles per super-tile (kernel template S)
   uint32_t grid = 0;
   uint32_t gap_nib0 = 0, first_start = 0;
   size_t lds = 0;
@@ -480,6 +606,8 @@ static void free_shard(gh_ctx* c) {
   (void)hipFree(c->d_gran);
   (void)hipFree(c->d_lut);
   (void)hipFree(c->d_fb);
+  (void)hipFree(c->d_stamps);
+  c->d_stamps = nullptr;
   c->d_payload = nullptr;
   c->d_gaps = nullptr;
   c->d_out = nullptr;
@@ -513,8 +641,10 @@ extern "C" int gh_ctx_create(int device, gh_ctx** out) {
   GH_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   GH_HIP(hipMalloc(&c->d_misc, 64));
   GH_HIP(hipMemset(c->d_misc, 0, 64));
-  GH_HIP(hipFuncSetAttribute((const void*)gh_decode_kernel,
-                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  for (int sv : {1, 2, 4, 8})
+    (void)hipFuncSetAttribute(kernel_for(sv), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+  (void)hipGetLastError();
   *out = c;
   return GH_OK;
 }
@@ -548,7 +678,6 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
   c->seg_begin = b;
   c->seg_end = e;
   c->n_total = s->n;
-  c->ntiles = (uint32_t)ceil_div(c->nseg, TB);
   if (c->nseg > 0) {
     const char* envk = getenv("GH_LUT_BITS");
     rc = build_tables(c->canon, c->tables, envk ? atoi(envk) : 0);
@@ -559,10 +688,10 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
   c->out_cap = out_cap;
   GH_HIP(hipSetDevice(c->device));
   GH_HIP(hipMalloc(&c->d_out, std::max<uint64_t>(out_cap, 16) + 64));
-  GH_HIP(hipMalloc(&c->d_gran, 8ull * std::max<uint32_t>(c->ntiles, 1)));
-  GH_HIP(hipMemset(c->d_gran, 0, 8ull * std::max<uint32_t>(c->ntiles, 1)));
   GH_HIP(hipMemset(c->d_misc, 0, 64));
   c->epoch = 0;
+  c->ntiles = 0;
+  c->grid = 0;
   if (c->nseg > 0) {
     const size_t lut_bytes = c->tables.lut.size() * sizeof(uint2);
     GH_HIP(hipMalloc(&c->d_lut, std::max<size_t>(lut_bytes, 16)));
@@ -570,12 +699,34 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
     GH_HIP(hipMalloc(&c->d_fb, sizeof(c->tables.fb)));
     GH_HIP(hipMemcpy(c->d_fb, c->tables.fb, sizeof(c->tables.fb), hipMemcpyHostToDevice));
     c->stage_bytes = (uint32_t)(((uint64_t)TB * c->tables.maxsyms_seg + 32 + 15) & ~15ull);
-    c->lds = lut_bytes + FB_BYTES + IN_BYTES + c->stage_bytes + SCRATCH_BYTES;
-    int per_cu = 0;
-    GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gh_decode_kernel, TB, c->lds));
-    if (per_cu < 1) return fail(GH_E_HIP, "decode kernel does not fit on a CU");
-    c->grid = (uint32_t)std::min<uint64_t>(c->ntiles, (uint64_t)per_cu * c->num_cu);
+    c->lds = lut_bytes + FB_BYTES + SLOT_BYTES + c->stage_bytes + SCRATCH_BYTES;
+    // Super-tile size: the largest S that still leaves every workgroup >= 4
+    // super-tiles (amortises ticket/load/look-back latency without a long tail).
+    const char* envs = getenv("GH_SUPER");
+    const int forced = envs ? atoi(envs) : 0;
+    c->super = 1;
+    for (int sv : {8, 4, 2, 1}) {
+      if (forced && sv != forced) continue;
+      int per_cu = 0;
+      GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_for(sv), TB, c->lds));
+      if (per_cu < 1) continue;
+      const uint64_t grid = (uint64_t)per_cu * c->num_cu;
+      const uint64_t ns = ceil_div(c->nseg, (uint64_t)sv * TB);
+      if (forced || ns >= 4 * grid || sv == 1) {
+        c->super = (uint32_t)sv;
+        c->ntiles = (uint32_t)ns;
+        c->grid = (uint32_t)std::min<uint64_t>(ns, grid);
+        break;
+      }
+    }
+    if (c->grid == 0) return fail(GH_E_HIP, "decode kernel does not fit on a CU");
+#ifdef GH_STAMPS
+    GH_HIP(hipMalloc(&c->d_stamps, 16ull * 8 * c->grid));
+    GH_HIP(hipMemset(c->d_stamps, 0, 16ull * 8 * c->grid));
+#endif
   }
+  GH_HIP(hipMalloc(&c->d_gran, 8ull * std::max<uint32_t>(c->ntiles, 1)));
+  GH_HIP(hipMemset(c->d_gran, 0, 8ull * std::max<uint32_t>(c->ntiles, 1)));
   // start bit of local segment 0, and the gap nibble base for the rest
   c->first_start = 0;
   if (b > 0) {
@@ -687,13 +838,14 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
   p.nseg = c->nseg;
   p.gap_nib0 = c->gap_nib0;
   p.first_start = c->first_start;
-  p.ntiles = c->ntiles;
+  p.nsuper = c->ntiles;
   p.kbits = c->tables.K;
   p.epoch = c->epoch;
   p.lut_bytes = (uint32_t)(c->tables.lut.size() * sizeof(uint2));
   p.stage_bytes = c->stage_bytes;
   p.fb_lo = c->tables.fb_lo;
   p.fb_hi = c->tables.fb_hi;
+  p.stamps = c->d_stamps;
   std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
   if (timed) {
     if (!c->pool.empty()) {
@@ -705,7 +857,12 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     }
     GH_HIP(hipEventRecord(ev.first, st));
   }
-  hipLaunchKernelGGL(gh_decode_kernel, dim3(c->grid), dim3(TB), c->lds, st, p);
+  switch (c->super) {
+    case 8: hipLaunchKernelGGL(gh_decode_kernel<8>, dim3(c->grid), dim3(TB), c->lds, st, p); break;
+    case 4: hipLaunchKernelGGL(gh_decode_kernel<4>, dim3(c->grid), dim3(TB), c->lds, st, p); break;
+    case 2: hipLaunchKernelGGL(gh_decode_kernel<2>, dim3(c->grid), dim3(TB), c->lds, st, p); break;
+    default: hipLaunchKernelGGL(gh_decode_kernel<1>, dim3(c->grid), dim3(TB), c->lds, st, p); break;
+  }
   GH_HIP(hipGetLastError());
   if (timed) {
     GH_HIP(hipEventRecord(ev.second, st));
@@ -833,3 +990,14 @@ extern "C" int gh_decode(const gh_stream* s, uint8_t* out, uint64_t out_len, con
   if (status & GH_ST_BADCODE) return fail(GH_E_CORRUPT, "invalid code in stream");
   return GH_OK;
 }
+
+#ifdef GH_STAMPS
+// Diagnostic build only: per-block phase cycle totals of the last launch.
+extern "C" int gh_debug_stamps(gh_ctx* c, unsigned long long* host, uint32_t max_blocks) {
+  if (!c || !host || !c->d_stamps) return fail(GH_E_ARG, "no stamps");
+  const uint32_t nb = std::min(max_blocks, c->grid);
+  GH_HIP(hipDeviceSynchronize());
+  GH_HIP(hipMemcpy(host, c->d_stamps, 16ull * 8 * nb, hipMemcpyDeviceToHost));
+  return (int)nb;
+}
+#endif
