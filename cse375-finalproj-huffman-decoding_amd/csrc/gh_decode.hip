@@ -46,9 +46,8 @@ constexpr int FB_WORDS = 3 * 17 + 64;    // limit16/base16/first + 256 symbol by
 constexpr int FB_BYTES = ((4 * FB_WORDS) + 15) & ~15;
 constexpr int MAX_SUPER = 8;             // sub-tiles per super-tile (template values 1,2,4,8)
 constexpr int SCRATCH_BYTES = 4 * (MAX_SUPER * NWAVE + 8);
-constexpr int SLOT_BYTES = 40 * TB;
 constexpr uint32_t EPOCH_MAX = (1u << 24) - 1;
-constexpr uint32_t SPIN_LIMIT = 1u << 22;
+constexpr uint32_t SPIN_LIMIT = 1u << 18;
 
 struct DecodeParams {
   const uint32_t* payload;       // local segment j owns words [4j, 4j+4); +1 look-ahead, zero padded
@@ -87,10 +86,17 @@ struct DecodeParams {
 #endif
 
 // ---- meta word of a LUT entry -------------------------------------------------
-//  [2:0] n symbols (0 = fallback), [7:3] bits consumed, [11:8] e1, [15:12] e2,
-//  [19:16] e3: end of symbol k = start of symbol k+1 (15 when absent).
-__device__ __forceinline__ uint32_t meta_n(uint32_t m) { return m & 7u; }
-__device__ __forceinline__ uint32_t meta_b(uint32_t m) { return (m >> 3) & 31u; }
+//  [4:0]   (32 - b) & 31: the v_alignbit amount that advances the window by b bits
+//  [12:8]  b, bits consumed (0 for a fallback entry)
+//  [18:16] n, symbols decoded (0 = codeword longer than K or invalid: fallback)
+//  [23:20] e1, [27:24] e2, [31:28] e3: end of symbol k = start of symbol k+1
+//          (15 when absent); used to drop symbols that start past the segment.
+__device__ __forceinline__ uint32_t meta_n(uint32_t m) { return (m >> 16) & 7u; }
+__device__ __forceinline__ uint32_t meta_b(uint32_t m) { return (m >> 8) & 31u; }
+__host__ __device__ constexpr uint32_t make_meta(uint32_t n, uint32_t b, uint32_t e1,
+                                                 uint32_t e2, uint32_t e3) {
+  return ((32u - b) & 31u) | (b << 8) | (n << 16) | (e1 << 20) | (e2 << 24) | (e3 << 28);
+}
 
 // Canonical decode of a codeword longer than the LUT width (rare).  Returns
 // (symbol << 8) | length; a pattern outside the code space sets GH_ST_BADCODE and
@@ -115,88 +121,158 @@ __device__ __forceinline__ uint32_t fallback_meta(const uint32_t* fb, uint32_t t
                                                   const DecodeParams& p, uint32_t* syms) {
   const uint32_t r = fallback_decode(fb, t >> 16, p.fb_lo, p.fb_hi, p.status);
   *syms = r >> 8;
-  return 1u | ((r & 31u) << 3) | 0xFFF00u;
+  return make_meta(1, r & 31u, 15, 15, 15);
 }
 
 // Symbols of the final lookup that start before the segment end (rem bits left).
 __device__ __forceinline__ uint32_t kept_in_last(uint32_t meta, int rem) {
   const uint32_t r = (uint32_t)min(rem, 15);
-  return 1u + (((meta >> 8) & 15u) < r) + (((meta >> 12) & 15u) < r) +
-         (((meta >> 16) & 15u) < r);
+  return 1u + (((meta >> 20) & 15u) < r) + (((meta >> 24) & 15u) < r) + ((meta >> 28) < r);
 }
 
-// Per-thread LDS slot (40 bytes, stride chosen so a wave's ds_read_b64 hits
-// distinct banks): the four overlapping word pairs {w[q], w[q+1]}, q = 0..3.
-// The 32-bit stream window at segment bit P is hi32(pair[P>>5] << (P&31)): one
-// 8-byte LDS read and a 64-bit shift, no shift-by-32 case.
-constexpr int SLOT_U64 = 5;  // 4 pairs + 1 pad (40 B)
-struct Seg {
-  uint32_t w[5];
-  int start;
+// The segment's bits live in a 160-bit funnel register d[0..4] (d[0] = the next
+// 32 stream bits, MSB first).  Consuming b bits (1..16) is four v_alignbit with
+// the LUT entry itself as the shift operand (alignbit reads its low 5 bits =
+// 32-b) plus one shift: no shift-by-32 case and no LDS window.
+// Starting at bit s <= 15 the register holds >= 145 valid bits, enough for the
+// last codeword (ends by bit 143) and its lookahead.
+struct Win {
+  uint32_t d0, d1, d2, d3, d4;
 };
 
-__device__ __forceinline__ void put_slot(unsigned long long* slot, const Seg& sg) {
+__device__ __forceinline__ Win make_win(uint4 w, uint32_t w4, int s) {
+  Win v;
+  const uint32_t sh = (uint32_t)(32 - s);
+  const bool z = (s == 0);
+  v.d0 = z ? w.x : __builtin_amdgcn_alignbit(w.x, w.y, sh);
+  v.d1 = z ? w.y : __builtin_amdgcn_alignbit(w.y, w.z, sh);
+  v.d2 = z ? w.z : __builtin_amdgcn_alignbit(w.z, w.w, sh);
+  v.d3 = z ? w.w : __builtin_amdgcn_alignbit(w.w, w4, sh);
+  v.d4 = w4 << s;
+  return v;
+}
+
+__device__ __forceinline__ void consume(Win& v, uint32_t meta) {
+  v.d0 = __builtin_amdgcn_alignbit(v.d0, v.d1, meta);
+  v.d1 = __builtin_amdgcn_alignbit(v.d1, v.d2, meta);
+  v.d2 = __builtin_amdgcn_alignbit(v.d2, v.d3, meta);
+  v.d3 = __builtin_amdgcn_alignbit(v.d3, v.d4, meta);
+  v.d4 = v.d4 << meta_b(meta);
+}
+
+// Count pass over U segments per thread, walked in lock-step so the U LUT reads
+// of an iteration are independent (ILP hides the LDS latency).  All U reads are
+// issued before anything consumes them; the rare fallback is one branch for all
+// chains so it does not split the read group.
+template <int U>
+__device__ __forceinline__ void count_segments(Win (&v)[U], const int (&start)[U],
+                                               const bool (&act)[U], uint32_t (&cnt)[U],
+                                               const uint32_t* s_lut32, const uint32_t* fb,
+                                               uint32_t kshift, const DecodeParams& p) {
+  int P[U], Plast[U];
+  uint32_t mlast[U];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) slot[q] = ((unsigned long long)sg.w[q] << 32) | sg.w[q + 1];
-}
-
-__device__ __forceinline__ uint32_t window32(const unsigned long long* slot, int P) {
-  return (uint32_t)((slot[P >> 5] << (P & 31)) >> 32);
-}
-
-__device__ __forceinline__ uint32_t count_segment(const unsigned long long* slot, int start,
-                                                  const uint32_t* s_lut32, const uint32_t* fb,
-                                                  uint32_t kshift, const DecodeParams& p) {
-  uint32_t cnt = 0, mlast = 0;
-  int P = start, Plast = start;
+  for (int u = 0; u < U; ++u) {
+    P[u] = act[u] ? start[u] : 128;
+    Plast[u] = P[u];
+    mlast[u] = make_meta(1, 0, 15, 15, 15);
+    cnt[u] = 0;
+  }
+  bool any;
   do {
-    const uint32_t t = window32(slot, P);
-    uint32_t meta = s_lut32[2 * (t >> kshift) + 1];
-    if (meta_n(meta) == 0) {
-      uint32_t sy;
-      meta = fallback_meta(fb, t, p, &sy);
+    uint32_t meta[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) meta[u] = s_lut32[2 * (v[u].d0 >> kshift) + 1];
+    bool need = false;
+#pragma unroll
+    for (int u = 0; u < U; ++u) need |= (meta_n(meta[u]) == 0) & (P[u] < 128);
+    if (need) {
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (meta_n(meta[u]) == 0 && P[u] < 128) {
+          uint32_t sy;
+          meta[u] = fallback_meta(fb, v[u].d0, p, &sy);
+        }
     }
-    cnt += meta_n(meta);
-    Plast = P;
-    mlast = meta;
-    P += (int)meta_b(meta);
-  } while (P < 128);
-  return cnt - (meta_n(mlast) - kept_in_last(mlast, 128 - Plast));
+    any = false;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool live = P[u] < 128;
+      cnt[u] += live ? meta_n(meta[u]) : 0u;
+      Plast[u] = live ? P[u] : Plast[u];
+      mlast[u] = live ? meta[u] : mlast[u];
+      P[u] += (int)meta_b(meta[u]);
+      consume(v[u], meta[u]);
+      any |= P[u] < 128;
+    }
+  } while (any);
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (act[u]) cnt[u] -= meta_n(mlast[u]) - kept_in_last(mlast[u], 128 - Plast[u]);
 }
 
-// Decode the segment again and OR its bytes into the LDS staging buffer starting at
-// byte `bpos`.  A word is flushed only once a later lookup starts, so the final
-// (possibly truncated) lookup's bytes are masked before they reach LDS.
-__device__ __forceinline__ void emit_segment(const unsigned long long* slot, int start,
-                                             const uint2* s_lut, const uint32_t* fb,
-                                             uint32_t kshift, const DecodeParams& p,
-                                             uint32_t* stg, uint32_t bpos) {
-  uint32_t oidx = bpos >> 2;
-  uint32_t fill = 8u * (bpos & 3u);
-  unsigned long long acc = 0;
-  uint32_t mlast = 0;
-  int P = start, Plast = start;
+// Emit pass: decode again and OR the bytes into the LDS staging buffer starting at
+// byte bpos[u].  A word is flushed only once a later lookup of the same segment
+// starts, so the final (possibly truncated) lookup's bytes are masked first.
+// Book-keeping is predicated (v_cndmask), only the LDS OR is a branch.
+template <int U>
+__device__ __forceinline__ void emit_segments(Win (&v)[U], const int (&start)[U],
+                                              const bool (&act)[U], const uint32_t (&bpos)[U],
+                                              const uint2* s_lut, const uint32_t* fb,
+                                              uint32_t kshift, const DecodeParams& p,
+                                              uint32_t* stg) {
+  int P[U], Plast[U];
+  uint32_t mlast[U], oidx[U], fill[U];
+  unsigned long long acc[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    P[u] = act[u] ? start[u] : 128;
+    Plast[u] = P[u];
+    mlast[u] = make_meta(1, 0, 15, 15, 15);
+    oidx[u] = bpos[u] >> 2;
+    fill[u] = 8u * (bpos[u] & 3u);
+    acc[u] = 0;
+  }
+  bool any;
   do {
-    const uint32_t t = window32(slot, P);
-    const uint2 e = s_lut[t >> kshift];
-    uint32_t meta = e.y, syms = e.x;
-    if (meta_n(meta) == 0) meta = fallback_meta(fb, t, p, &syms);
-    if (fill >= 32) {
-      atomicOr(&stg[oidx], (uint32_t)acc);
-      acc >>= 32;
-      fill -= 32;
-      ++oidx;
+    uint2 e[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) e[u] = s_lut[v[u].d0 >> kshift];
+    bool need = false;
+#pragma unroll
+    for (int u = 0; u < U; ++u) need |= (meta_n(e[u].y) == 0) & (P[u] < 128);
+    if (need) {
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (meta_n(e[u].y) == 0 && P[u] < 128) e[u].y = fallback_meta(fb, v[u].d0, p, &e[u].x);
     }
-    acc |= (unsigned long long)syms << fill;
-    fill += 8u * meta_n(meta);
-    Plast = P;
-    mlast = meta;
-    P += (int)meta_b(meta);
-  } while (P < 128);
-  fill -= 8u * (meta_n(mlast) - kept_in_last(mlast, 128 - Plast));
-  acc &= (1ull << fill) - 1ull;  // fill < 64
-  if (fill > 0) atomicOr(&stg[oidx], (uint32_t)acc);
-  if (fill > 32) atomicOr(&stg[oidx + 1], (uint32_t)(acc >> 32));
+    any = false;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool live = P[u] < 128;
+      const uint32_t meta = e[u].y;
+      const bool flush = live && fill[u] >= 32;
+      if (flush) atomicOr(&stg[oidx[u]], (uint32_t)acc[u]);
+      acc[u] = flush ? (acc[u] >> 32) : acc[u];
+      fill[u] -= flush ? 32u : 0u;
+      oidx[u] += flush ? 1u : 0u;
+      acc[u] |= live ? ((unsigned long long)e[u].x << fill[u]) : 0ull;
+      fill[u] += live ? 8u * meta_n(meta) : 0u;
+      Plast[u] = live ? P[u] : Plast[u];
+      mlast[u] = live ? meta : mlast[u];
+      P[u] += (int)meta_b(meta);
+      consume(v[u], meta);
+      any |= P[u] < 128;
+    }
+  } while (any);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (!act[u]) continue;
+    uint32_t f = fill[u] - 8u * (meta_n(mlast[u]) - kept_in_last(mlast[u], 128 - Plast[u]));
+    const unsigned long long a = acc[u] & ((1ull << f) - 1ull);  // f < 64
+    if (f > 0) atomicOr(&stg[oidx[u]], (uint32_t)a);
+    if (f > 32) atomicOr(&stg[oidx[u] + 1], (uint32_t)(a >> 32));
+  }
 }
 
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
@@ -222,23 +298,23 @@ __device__ __forceinline__ unsigned long long granule(unsigned epoch, unsigned f
          (v & ((1ull << 38) - 1));
 }
 
-// Decoupled look-back by one wave: publishes the aggregate, sums predecessors'
-// aggregates back to the nearest inclusive prefix (256 granules per round: lane l
-// reads distances l, l+64, l+128, l+192), publishes the inclusive prefix and
-// returns the exclusive one.  Predecessors hold earlier tickets, so they are
-// running and the spin terminates (bounded anyway by SPIN_LIMIT).
-__device__ unsigned long long look_back(const DecodeParams& p, uint32_t tile,
-                                        unsigned long long total, int lane) {
+// Decoupled look-back, split so that publishing the aggregate (right after the
+// count) and resolving the prefix (one tile later) are separate steps.  Resolve:
+// one wave sums predecessors' aggregates back to the nearest inclusive prefix
+// (256 granules per round: lane l reads distances l, l+64, l+128, l+192),
+// publishes the inclusive prefix and returns the exclusive one.  Every predecessor
+// publishes its aggregate right after counting, without waiting on anything, so
+// the spin terminates (bounded anyway by SPIN_LIMIT).
+__device__ __forceinline__ void publish_aggregate(const DecodeParams& p, uint32_t tile,
+                                                  unsigned long long total) {
+  __hip_atomic_store(&p.granules[tile], granule(p.epoch, tile == 0 ? 2 : 1, total),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ unsigned long long resolve_prefix(const DecodeParams& p, uint32_t tile,
+                                             unsigned long long total, int lane) {
   constexpr unsigned long long VMASK = (1ull << 38) - 1;
-  if (tile == 0) {
-    if (lane == 0)
-      __hip_atomic_store(&p.granules[0], granule(p.epoch, 2, total), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    return 0;
-  }
-  if (lane == 0)
-    __hip_atomic_store(&p.granules[tile], granule(p.epoch, 1, total), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
+  if (tile == 0) return 0;
   unsigned long long excl = 0;
   long long base = (long long)tile - 1;
   uint32_t spins = 0;
@@ -257,8 +333,7 @@ __device__ unsigned long long look_back(const DecodeParams& p, uint32_t tile,
     for (int j = 0; j < 4; ++j)
       if (base - lane - 64 * j >= 0)
         st[j] = ((uint32_t)(g[j] >> 40) == p.epoch) ? (uint32_t)((g[j] >> 38) & 3u) : 0u;
-    // nearest inclusive prefix: distance d = 64*j + lane
-    int fp = 256;
+    int fp = 256;  // nearest inclusive prefix: distance d = 64*j + lane
 #pragma unroll
     for (int j = 3; j >= 0; --j) {
       const unsigned long long pm = __ballot(st[j] == 2);
@@ -272,7 +347,7 @@ __device__ unsigned long long look_back(const DecodeParams& p, uint32_t tile,
         if (lane == 0) atomicOr(p.status, (unsigned)GH_ST_TIMEOUT);
         break;
       }
-      __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_s_sleep(2);
       continue;
     }
     unsigned long long v = 0;
@@ -315,23 +390,49 @@ __device__ __forceinline__ void copy_out(const DecodeParams& p, uint4* st, unsig
   }
 }
 
-// One workgroup processes super-tiles of S*TB segments, drawn from an atomic ticket
-// (the next ticket is prefetched while the current super-tile runs):
-//   1. load the S segments of each thread into registers (16-byte loads);
-//   2. count every segment (LUT-driven walk), scan the S sub-tiles, publish the
-//      super-tile aggregate and run the look-back once;
-//   3. per sub-tile: decode again into LDS staging at the final byte alignment,
-//      then store the sub-tile with 16-byte stores.
-template <int S>
+// Load the U segments of a tile owned by this thread (16-byte loads, coalesced).
+template <int U>
+__device__ __forceinline__ void load_tile(const DecodeParams& p, uint32_t tile, int tid,
+                                          uint4 (&w)[U], uint32_t (&w4)[U], int (&start)[U],
+                                          bool (&act)[U]) {
+  const unsigned long long seg0 = (unsigned long long)tile * (U * TB) + tid;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const unsigned long long seg = seg0 + (unsigned long long)u * TB;
+    act[u] = seg < p.nseg;
+    start[u] = 0;
+    w[u] = make_uint4(0, 0, 0, 0);
+    w4[u] = 0;
+    if (act[u]) {
+      w[u] = *(const uint4*)(p.payload + 4 * seg);
+      w4[u] = p.payload[4 * seg + 4];
+      if (seg == 0) {
+        start[u] = (int)p.first_start;
+      } else {
+        const unsigned long long nib = (unsigned long long)p.gap_nib0 + seg - 1;
+        start[u] = (int)((p.gaps[nib >> 3] >> (4 * (nib & 7))) & 15u);
+      }
+    }
+  }
+}
+
+// One workgroup processes tiles of U*TB segments (thread t owns segments
+// tile*U*TB + u*TB + t) drawn from an atomic ticket.  Per iteration, with the
+// look-back of the previous tile deferred by one count phase:
+//   1. load + count the new tile (U segments per thread in lock-step), scan it
+//      and publish its aggregate at once;
+//   2. resolve the previous tile's prefix (its predecessors have had a whole
+//      count phase to publish), re-load its words (L2-resident), decode them into
+//      LDS staging at the final byte alignment and store with 16-byte stores.
+template <int U>
 __global__ __launch_bounds__(TB) void gh_decode_kernel(const DecodeParams p) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint2* s_lut = (uint2*)smem;
+  const uint2* s_lut = (const uint2*)smem;
   const uint32_t* s_lut32 = (const uint32_t*)smem;
   uint32_t* s_fb = (uint32_t*)(smem + p.lut_bytes);
-  unsigned long long* s_slots = (unsigned long long*)(smem + p.lut_bytes + FB_BYTES);
-  uint8_t* s_stage = smem + p.lut_bytes + FB_BYTES + SLOT_BYTES;
+  uint8_t* s_stage = smem + p.lut_bytes + FB_BYTES;
   uint32_t* s_scr = (uint32_t*)(s_stage + p.stage_bytes);
-  // scratch: [0, S*NWAVE) wave sums per sub-tile, [32] ticket, [34..35] super offset
+  // scratch: [0, 2*U*NWAVE) wave sums of two tiles, [32] ticket, [34..35] offset
   uint32_t* s_ticket = s_scr + MAX_SUPER * NWAVE;
   unsigned long long* s_goff = (unsigned long long*)(s_scr + MAX_SUPER * NWAVE + 2);
 
@@ -339,7 +440,6 @@ __global__ __launch_bounds__(TB) void gh_decode_kernel(const DecodeParams p) {
   const int lane = tid & 63;
   const int wid = tid >> 6;
 
-  // Stage the decode tables in LDS once per persistent workgroup.
   {
     const uint4* g = p.lut;
     uint4* s = (uint4*)smem;
@@ -352,110 +452,112 @@ __global__ __launch_bounds__(TB) void gh_decode_kernel(const DecodeParams p) {
   __syncthreads();
 
   const uint32_t kshift = 32u - p.kbits;
-  unsigned long long* slot = s_slots + SLOT_U64 * tid;
   STAMP_DECL
 
-  for (;;) {
+  bool have_prev = false;
+  uint32_t prev = 0, prev_total = 0, parity = 0;
+  uint32_t prev_bpos[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) prev_bpos[u] = 0;
+
+  for (uint32_t iter = 0;; ++iter) {
     STAMP(9);
     const uint32_t tile = *s_ticket;
-    if (tile >= p.nsuper) {
-      if (tid == 0 && tile == p.nsuper + gridDim.x - 1)
-        __hip_atomic_store(p.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool have_cur = tile < p.nsuper;
+    if (iter > p.nsuper + 1) {  // cannot happen; a guard so a logic error never hangs the GPU
+      if (tid == 0) atomicOr(p.status, (unsigned)GH_ST_TIMEOUT);
       break;
     }
-    uint32_t next = 0;
-    if (tid == 0) next = atomicAdd(p.ticket, 1u);  // consumed at the end of this tile
+    if (!have_cur && tid == 0 && tile == p.nsuper + gridDim.x - 1)
+      __hip_atomic_store(p.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!have_cur && !have_prev) break;
 
-    // ---- 1. load S segments per thread -------------------------------------------
-    Seg sg[S];
-    bool act[S];
-    const unsigned long long seg0 = (unsigned long long)tile * (S * TB) + tid;
+    // ---- 1. new tile: load, count, scan, publish aggregate -------------------------
+    uint32_t cur_bpos[U];
+    uint32_t cur_total = 0;
+    uint32_t* sums = s_scr + parity * (U * NWAVE);
+    if (have_cur) {
+      uint4 w[U];
+      uint32_t w4[U];
+      int start[U];
+      bool act[U];
+      load_tile<U>(p, tile, tid, w, w4, start, act);
+      STAMP(0);
+      Win v[U];
 #pragma unroll
-    for (int s = 0; s < S; ++s) {
-      const unsigned long long seg = seg0 + (unsigned long long)s * TB;
-      act[s] = seg < p.nseg;
-      sg[s].start = 0;
-      if (act[s]) {
-        const uint4 w = *(const uint4*)(p.payload + 4 * seg);
-        sg[s].w[0] = w.x;
-        sg[s].w[1] = w.y;
-        sg[s].w[2] = w.z;
-        sg[s].w[3] = w.w;
-        sg[s].w[4] = p.payload[4 * seg + 4];
-        if (seg == 0) {
-          sg[s].start = (int)p.first_start;
-        } else {
-          const unsigned long long nib = (unsigned long long)p.gap_nib0 + seg - 1;
-          sg[s].start = (int)((p.gaps[nib >> 3] >> (4 * (nib & 7))) & 15u);
-        }
+      for (int u = 0; u < U; ++u) v[u] = make_win(w[u], w4[u], start[u]);
+      uint32_t cnt[U];
+      count_segments<U>(v, start, act, cnt, s_lut32, s_fb, kshift, p);
+      STAMP(1);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t incl = wave_incl_scan(cnt[u], lane);
+        if (lane == 63) sums[u * NWAVE + wid] = incl;
+        cur_bpos[u] = incl - cnt[u];
       }
-    }
-    STAMP(0);
-
-    // ---- 2. count, scan, look-back --------------------------------------------------
-    uint32_t cnt[S];
-#pragma unroll
-    for (int s = 0; s < S; ++s) {
-      cnt[s] = 0;
-      if (act[s]) {
-        put_slot(slot, sg[s]);
-        cnt[s] = count_segment(slot, sg[s].start, s_lut32, s_fb, kshift, p);
-      }
-    }
-    STAMP(1);
-    uint32_t excl[S];
-#pragma unroll
-    for (int s = 0; s < S; ++s) {
-      const uint32_t incl = wave_incl_scan(cnt[s], lane);
-      if (lane == 63) s_scr[s * NWAVE + wid] = incl;
-      excl[s] = incl - cnt[s];
     }
     __syncthreads();
     STAMP(2);
-    unsigned long long super_total = 0;
+    if (have_cur) {
 #pragma unroll
-    for (int s = 0; s < S; ++s) {
+      for (int u = 0; u < U; ++u) {
+        const uint32_t before = cur_total;
 #pragma unroll
-      for (int w = 0; w < NWAVE; ++w) {
-        const uint32_t v = s_scr[s * NWAVE + w];
-        excl[s] += (w < wid) ? v : 0u;
-        super_total += v;
+        for (int q = 0; q < NWAVE; ++q) {
+          const uint32_t x = sums[u * NWAVE + q];
+          cur_bpos[u] += (q < wid) ? x : 0u;
+          cur_total += x;
+        }
+        cur_bpos[u] += before;
       }
+      if (tid == 0) publish_aggregate(p, tile, cur_total);
     }
-    if (wid == 0) {
-      const unsigned long long ex = look_back(p, tile, super_total, lane);
-      if (lane == 0) {
-        *s_goff = ex;
-        if (tile == p.nsuper - 1) *p.total = ex + super_total;
-      }
-    }
-    STAMP(3);
-    __syncthreads();
-    STAMP(4);
 
-    // ---- 3. per sub-tile: decode into staging, store -------------------------------
-    unsigned long long goff = *s_goff;
-    uint32_t* stg = (uint32_t*)s_stage;
-#pragma unroll
-    for (int s = 0; s < S; ++s) {
-      uint32_t sub_total = 0;
-#pragma unroll
-      for (int w = 0; w < NWAVE; ++w) sub_total += s_scr[s * NWAVE + w];
-      if (act[s]) {
-        put_slot(slot, sg[s]);
-        emit_segment(slot, sg[s].start, s_lut, s_fb, kshift, p, stg, (uint32_t)(goff & 15) + excl[s]);
+    // ---- 2. previous tile: resolve prefix, emit, store ---------------------------------
+    if (have_prev) {
+      uint4 w[U];
+      uint32_t w4[U];
+      int start[U];
+      bool act[U];
+      load_tile<U>(p, prev, tid, w, w4, start, act);  // L2-resident re-read
+      if (wid == 0) {
+        const unsigned long long ex = resolve_prefix(p, prev, prev_total, lane);
+        if (lane == 0) {
+          *s_goff = ex;
+          if (prev == p.nsuper - 1) *p.total = ex + prev_total;
+        }
       }
+      STAMP(3);
+      __syncthreads();
+      STAMP(4);
+      if (tid == 0)  // next tile, drawn before the emit; none after the first out-of-range one
+        *s_ticket = have_cur ? atomicAdd(p.ticket, 1u) : 0xFFFFFFFFu;
+      const unsigned long long goff = *s_goff;
+      const uint32_t lb = (uint32_t)(goff & 15);
+      Win v[U];
+      uint32_t bpos[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        v[u] = make_win(w[u], w4[u], start[u]);
+        bpos[u] = prev_bpos[u] + lb;
+      }
+      emit_segments<U>(v, start, act, bpos, s_lut, s_fb, kshift, p, (uint32_t*)s_stage);
       STAMP(5);
       __syncthreads();
       STAMP(6);
-      copy_out(p, (uint4*)s_stage, goff, sub_total, tid);
-      goff += sub_total;
+      copy_out(p, (uint4*)s_stage, goff, prev_total, tid);
       STAMP(7);
-      __syncthreads();
-      STAMP(8);
+    } else {
+      if (tid == 0) *s_ticket = have_cur ? atomicAdd(p.ticket, 1u) : 0xFFFFFFFFu;
     }
-    if (tid == 0) *s_ticket = next;
     __syncthreads();
+    STAMP(8);
+    have_prev = have_cur;
+    prev = tile;
+    prev_total = cur_total;
+#pragma unroll
+    for (int u = 0; u < U; ++u) prev_bpos[u] = cur_bpos[u];
+    parity ^= 1u;
   }
   STAMP_FLUSH;
 }
@@ -486,9 +588,8 @@ static uint32_t lut_meta_for(const Canon& c, uint32_t idx, uint32_t K, uint32_t*
     ends[n] = pos;
   }
   *syms = s;
-  uint32_t meta = n | (pos << 3);
-  for (uint32_t k = 1; k <= 3; ++k) meta |= ((k < n) ? ends[k] : 15u) << (4 + 4 * k);
-  return meta;
+  if (n == 0) return make_meta(0, 0, 15, 15, 15);
+  return make_meta(n, pos, 1 < n ? ends[1] : 15u, 2 < n ? ends[2] : 15u, 3 < n ? ends[3] : 15u);
 }
 
 // Expected lookups per symbol for width K under the code's own model (P(code) =
@@ -503,11 +604,12 @@ static uint32_t choose_k(const Canon& c) {
     for (uint32_t i = 0; i < (1u << K); ++i) {
       uint32_t s;
       const uint32_t m = lut_meta_for(c, i, K, &s);
-      if ((m & 7) == 0) {
+      const uint32_t n = (m >> 16) & 7u;
+      if (n == 0) {
         fbp += 1.0;
         syms += 1.0;
       } else {
-        syms += (m & 7);
+        syms += n;
       }
     }
     syms /= (double)(1u << K);
@@ -560,9 +662,8 @@ using namespace gh;
       return fail(GH_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));   \
   } while (0)
 
-static const void* kernel_for(int sv) {
-  switch (sv) {
-    case 8: return (const void*)gh_decode_kernel<8>;
+static const void* kernel_for(int uv) {
+  switch (uv) {
     case 4: return (const void*)gh_decode_kernel<4>;
     case 2: return (const void*)gh_decode_kernel<2>;
     default: return (const void*)gh_decode_kernel<1>;
@@ -641,7 +742,7 @@ extern "C" int gh_ctx_create(int device, gh_ctx** out) {
   GH_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   GH_HIP(hipMalloc(&c->d_misc, 64));
   GH_HIP(hipMemset(c->d_misc, 0, 64));
-  for (int sv : {1, 2, 4, 8})
+  for (int sv : {1, 2, 4})
     (void)hipFuncSetAttribute(kernel_for(sv), hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
   (void)hipGetLastError();
@@ -698,26 +799,22 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
     GH_HIP(hipMemcpy(c->d_lut, c->tables.lut.data(), lut_bytes, hipMemcpyHostToDevice));
     GH_HIP(hipMalloc(&c->d_fb, sizeof(c->tables.fb)));
     GH_HIP(hipMemcpy(c->d_fb, c->tables.fb, sizeof(c->tables.fb), hipMemcpyHostToDevice));
-    c->stage_bytes = (uint32_t)(((uint64_t)TB * c->tables.maxsyms_seg + 32 + 15) & ~15ull);
-    c->lds = lut_bytes + FB_BYTES + SLOT_BYTES + c->stage_bytes + SCRATCH_BYTES;
-    // Super-tile size: the largest S that still leaves every workgroup >= 4
-    // super-tiles (amortises ticket/load/look-back latency without a long tail).
-    const char* envs = getenv("GH_SUPER");
-    const int forced = envs ? atoi(envs) : 0;
-    c->super = 1;
-    for (int sv : {8, 4, 2, 1}) {
-      if (forced && sv != forced) continue;
-      int per_cu = 0;
-      GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_for(sv), TB, c->lds));
-      if (per_cu < 1) continue;
+    // Segments per thread (ILP): as many as keep the tile's staging <= 32 KiB.
+    const char* envu = getenv("GH_U");
+    int uv = envu ? atoi(envu) : 0;
+    if (uv != 1 && uv != 2 && uv != 4) {
+      const uint32_t per = TB * c->tables.maxsyms_seg;
+      uv = (4 * per <= 32768) ? 4 : (2 * per <= 32768) ? 2 : 1;
+    }
+    c->super = (uint32_t)uv;
+    c->stage_bytes = (uint32_t)(((uint64_t)uv * TB * c->tables.maxsyms_seg + 32 + 15) & ~15ull);
+    c->lds = lut_bytes + FB_BYTES + c->stage_bytes + SCRATCH_BYTES;
+    int per_cu = 0;
+    GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_for(uv), TB, c->lds));
+    if (per_cu >= 1) {
       const uint64_t grid = (uint64_t)per_cu * c->num_cu;
-      const uint64_t ns = ceil_div(c->nseg, (uint64_t)sv * TB);
-      if (forced || ns >= 4 * grid || sv == 1) {
-        c->super = (uint32_t)sv;
-        c->ntiles = (uint32_t)ns;
-        c->grid = (uint32_t)std::min<uint64_t>(ns, grid);
-        break;
-      }
+      c->ntiles = (uint32_t)ceil_div(c->nseg, (uint64_t)uv * TB);
+      c->grid = (uint32_t)std::min<uint64_t>(c->ntiles, grid);
     }
     if (c->grid == 0) return fail(GH_E_HIP, "decode kernel does not fit on a CU");
 #ifdef GH_STAMPS
@@ -858,7 +955,6 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     GH_HIP(hipEventRecord(ev.first, st));
   }
   switch (c->super) {
-    case 8: hipLaunchKernelGGL(gh_decode_kernel<8>, dim3(c->grid), dim3(TB), c->lds, st, p); break;
     case 4: hipLaunchKernelGGL(gh_decode_kernel<4>, dim3(c->grid), dim3(TB), c->lds, st, p); break;
     case 2: hipLaunchKernelGGL(gh_decode_kernel<2>, dim3(c->grid), dim3(TB), c->lds, st, p); break;
     default: hipLaunchKernelGGL(gh_decode_kernel<1>, dim3(c->grid), dim3(TB), c->lds, st, p); break;
