@@ -70,7 +70,13 @@ struct DecodeParams {
   unsigned int stage_bytes;
   unsigned int fb_lo, fb_hi;     // fallback length range
   unsigned long long* stamps;    // diagnostic build only (GH_STAMPS): per-block phase cycles
+  unsigned int ablate;           // diagnostic build only: 1 no resolve, 2 no copy-out, 4 no stage
 };
+#ifdef GH_STAMPS
+#define ABLATE(bit) (p.ablate & (bit))
+#else
+#define ABLATE(bit) 0
+#endif
 
 // Diagnostic phase stamps (compiled only with -DGH_STAMPS; never in the shipped
 // library): lane 0 of wave 0 accumulates s_memtime deltas per phase.
@@ -164,11 +170,12 @@ __device__ __forceinline__ void consume(Win& v, uint32_t meta) {
 // of an iteration are independent (ILP hides the LDS latency).  All U reads are
 // issued before anything consumes them; the rare fallback is one branch for all
 // chains so it does not split the read group.
-template <int U>
+template <bool FB, int U>
 __device__ __forceinline__ void count_segments(Win (&v)[U], const int (&start)[U],
                                                const bool (&act)[U], uint32_t (&cnt)[U],
                                                const uint32_t* s_lut32, const uint32_t* fb,
-                                               uint32_t kshift, const DecodeParams& p) {
+                                               uint32_t kshift, const DecodeParams& p,
+                                               uint32_t& bad) {
   int P[U], Plast[U];
   uint32_t mlast[U];
 #pragma unroll
@@ -183,25 +190,29 @@ __device__ __forceinline__ void count_segments(Win (&v)[U], const int (&start)[U
     uint32_t meta[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) meta[u] = s_lut32[2 * (v[u].d0 >> kshift) + 1];
-    bool need = false;
+    if constexpr (FB) {
+      bool need = false;
 #pragma unroll
-    for (int u = 0; u < U; ++u) need |= (meta_n(meta[u]) == 0) & (P[u] < 128);
-    if (need) {
+      for (int u = 0; u < U; ++u) need |= (meta_n(meta[u]) == 0) & (P[u] < 128);
+      if (need) {
 #pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (meta_n(meta[u]) == 0 && P[u] < 128) {
-          uint32_t sy;
-          meta[u] = fallback_meta(fb, v[u].d0, p, &sy);
-        }
+        for (int u = 0; u < U; ++u)
+          if (meta_n(meta[u]) == 0 && P[u] < 128) {
+            uint32_t sy;
+            meta[u] = fallback_meta(fb, v[u].d0, p, &sy);
+          }
+      }
     }
     any = false;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const bool live = P[u] < 128;
+      if constexpr (!FB) bad |= (live && meta_n(meta[u]) == 0) ? 1u : 0u;
       cnt[u] += live ? meta_n(meta[u]) : 0u;
       Plast[u] = live ? P[u] : Plast[u];
       mlast[u] = live ? meta[u] : mlast[u];
-      P[u] += (int)meta_b(meta[u]);
+      // an invalid pattern (no-fallback build) still advances so the loop ends
+      P[u] += FB ? (int)meta_b(meta[u]) : max((int)meta_b(meta[u]), 1);
       consume(v[u], meta[u]);
       any |= P[u] < 128;
     }
@@ -215,7 +226,7 @@ __device__ __forceinline__ void count_segments(Win (&v)[U], const int (&start)[U
 // byte bpos[u].  A word is flushed only once a later lookup of the same segment
 // starts, so the final (possibly truncated) lookup's bytes are masked first.
 // Book-keeping is predicated (v_cndmask), only the LDS OR is a branch.
-template <int U>
+template <bool FB, int U>
 __device__ __forceinline__ void emit_segments(Win (&v)[U], const int (&start)[U],
                                               const bool (&act)[U], const uint32_t (&bpos)[U],
                                               const uint2* s_lut, const uint32_t* fb,
@@ -238,21 +249,24 @@ __device__ __forceinline__ void emit_segments(Win (&v)[U], const int (&start)[U]
     uint2 e[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) e[u] = s_lut[v[u].d0 >> kshift];
-    bool need = false;
+    if constexpr (FB) {
+      bool need = false;
 #pragma unroll
-    for (int u = 0; u < U; ++u) need |= (meta_n(e[u].y) == 0) & (P[u] < 128);
-    if (need) {
+      for (int u = 0; u < U; ++u) need |= (meta_n(e[u].y) == 0) & (P[u] < 128);
+      if (need) {
 #pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (meta_n(e[u].y) == 0 && P[u] < 128) e[u].y = fallback_meta(fb, v[u].d0, p, &e[u].x);
+        for (int u = 0; u < U; ++u)
+          if (meta_n(e[u].y) == 0 && P[u] < 128) e[u].y = fallback_meta(fb, v[u].d0, p, &e[u].x);
+      }
     }
     any = false;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const bool live = P[u] < 128;
       const uint32_t meta = e[u].y;
+      // flush the word completed by earlier lookups (OR of 0 when none): no branch
       const bool flush = live && fill[u] >= 32;
-      if (flush) atomicOr(&stg[oidx[u]], (uint32_t)acc[u]);
+      atomicOr(&stg[oidx[u]], flush ? (uint32_t)acc[u] : 0u);
       acc[u] = flush ? (acc[u] >> 32) : acc[u];
       fill[u] -= flush ? 32u : 0u;
       oidx[u] += flush ? 1u : 0u;
@@ -260,7 +274,7 @@ __device__ __forceinline__ void emit_segments(Win (&v)[U], const int (&start)[U]
       fill[u] += live ? 8u * meta_n(meta) : 0u;
       Plast[u] = live ? P[u] : Plast[u];
       mlast[u] = live ? meta : mlast[u];
-      P[u] += (int)meta_b(meta);
+      P[u] += FB ? (int)meta_b(meta) : max((int)meta_b(meta), 1);
       consume(v[u], meta);
       any |= P[u] < 128;
     }
@@ -364,32 +378,6 @@ __device__ unsigned long long resolve_prefix(const DecodeParams& p, uint32_t til
   return excl;
 }
 
-// Copy one sub-tile's staged bytes [lbase, lbase+n) to out[goff, goff+n) clamped at
-// out_cap: 16-byte stores for whole chunks, byte stores for the two edge chunks;
-// zeroes the staging behind itself.
-__device__ __forceinline__ void copy_out(const DecodeParams& p, uint4* st, unsigned long long goff,
-                                         uint32_t n, int tid) {
-  const uint32_t lbase = (uint32_t)(goff & 15);
-  const unsigned long long a0 = goff - lbase;
-  const unsigned long long end = min(goff + n, p.out_cap);
-  const uint32_t nz = (lbase + n + 15u) >> 4;
-  for (uint32_t c = tid; c < nz; c += TB) {
-    const unsigned long long gs = a0 + 16ull * c;
-    const uint4 v = st[c];
-    st[c] = make_uint4(0, 0, 0, 0);
-    if (gs >= goff && gs + 16 <= end) {
-      *(uint4*)(p.out + gs) = v;
-    } else {
-      const uint8_t* b = (const uint8_t*)&v;
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const unsigned long long ga = gs + k;
-        if (ga >= goff && ga < end) p.out[ga] = b[k];
-      }
-    }
-  }
-}
-
 // Load the U segments of a tile owned by this thread (16-byte loads, coalesced).
 template <int U>
 __device__ __forceinline__ void load_tile(const DecodeParams& p, uint32_t tile, int tid,
@@ -416,23 +404,169 @@ __device__ __forceinline__ void load_tile(const DecodeParams& p, uint32_t tile, 
   }
 }
 
-// One workgroup processes tiles of U*TB segments (thread t owns segments
-// tile*U*TB + u*TB + t) drawn from an atomic ticket.  Per iteration, with the
-// look-back of the previous tile deferred by one count phase:
-//   1. load + count the new tile (U segments per thread in lock-step), scan it
-//      and publish its aggregate at once;
-//   2. resolve the previous tile's prefix (its predecessors have had a whole
-//      count phase to publish), re-load its words (L2-resident), decode them into
-//      LDS staging at the final byte alignment and store with 16-byte stores.
-template <int U>
+// ---------------------------------------------------------------------------
+// Single-symbol path (codes with minlen >= 4, where multi-symbol lookups buy
+// little, e.g. redundancy 0.1): ONE decode pass per segment.
+//  * LUT entry (u32): [4:0] (32-b)&31, [12:8] b, [31:24] symbol; b = 0 marks a
+//    codeword longer than K or an invalid pattern (fallback).
+//  * The step loop is fully unrolled (at most 128/4 = 32 steps, checked for a
+//    wave-wide exit every 4 steps), so step j's symbol goes to byte j of the
+//    register out[j/4] with one v_perm: static indices, no LDS, no count pass,
+//    and no truncation fixup (a lookup decodes exactly one codeword, which is
+//    kept iff it starts before bit 128).
+// ---------------------------------------------------------------------------
+constexpr int OW = 8;  // output words per segment (32 symbols)
+
+__device__ __forceinline__ uint32_t fallback_entry1(const uint32_t* fb, uint32_t t,
+                                                    const DecodeParams& p) {
+  const uint32_t r = fallback_decode(fb, t >> 16, p.fb_lo, p.fb_hi, p.status);
+  const uint32_t b = r & 31u;
+  return ((32u - b) & 31u) | (b << 8) | ((r >> 8) << 24);
+}
+
+// v_perm selector placing byte 3 of S0 (the symbol) at byte j, keeping S1's others.
+__device__ __forceinline__ constexpr uint32_t perm_sel(int j) {
+  return j == 0 ? 0x03020107u : j == 1 ? 0x03020700u : j == 2 ? 0x03070100u : 0x07020100u;
+}
+
+template <bool FB, int U>
+__device__ __forceinline__ void decode1_segments(Win (&v)[U], const int (&start)[U],
+                                                 const bool (&act)[U], uint32_t (&ow)[U][OW],
+                                                 uint32_t (&cnt)[U], const uint32_t* s_lut32,
+                                                 const uint32_t* fb, uint32_t kshift,
+                                                 const DecodeParams& p, uint32_t& bad) {
+  int P[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    P[u] = act[u] ? start[u] : 128;
+    cnt[u] = 0;
+#pragma unroll
+    for (int k = 0; k < OW; ++k) ow[u][k] = 0;
+  }
+#pragma unroll
+  for (int blk = 0; blk < OW; ++blk) {
+    bool live_any = false;
+#pragma unroll
+    for (int u = 0; u < U; ++u) live_any |= P[u] < 128;
+    if (!__any(live_any)) break;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uint32_t e[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) e[u] = s_lut32[v[u].d0 >> kshift];
+      if constexpr (FB) {
+        bool need = false;
+#pragma unroll
+        for (int u = 0; u < U; ++u) need |= ((e[u] & 0x1F00u) == 0) & (P[u] < 128);
+        if (need) {
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+            if ((e[u] & 0x1F00u) == 0 && P[u] < 128) e[u] = fallback_entry1(fb, v[u].d0, p);
+        }
+      } else {
+        // an invalid pattern: flag it and step one bit so the walk still ends
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const bool inval = (e[u] & 0x1F00u) == 0;
+          bad |= (inval && P[u] < 128) ? 1u : 0u;
+          e[u] = inval ? (31u | (1u << 8)) : e[u];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        ow[u][blk] = __builtin_amdgcn_perm(e[u], ow[u][blk], perm_sel(j));
+        cnt[u] += (P[u] < 128) ? 1u : 0u;
+        P[u] += (int)((e[u] >> 8) & 31u);
+        v[u].d0 = __builtin_amdgcn_alignbit(v[u].d0, v[u].d1, e[u]);
+        v[u].d1 = __builtin_amdgcn_alignbit(v[u].d1, v[u].d2, e[u]);
+        v[u].d2 = __builtin_amdgcn_alignbit(v[u].d2, v[u].d3, e[u]);
+        v[u].d3 = __builtin_amdgcn_alignbit(v[u].d3, v[u].d4, e[u]);
+        v[u].d4 = __builtin_amdgcn_alignbit(v[u].d4, 0u, e[u]);
+      }
+    }
+  }
+}
+
+// OR a segment's n output bytes (held in registers) into the staging buffer at
+// byte position pos.
+__device__ __forceinline__ void stage_bytes(uint32_t* stg, const uint32_t (&ow)[OW], uint32_t n,
+                                            uint32_t pos) {
+  const uint32_t s8 = 8u * (pos & 3u);
+  const uint32_t w0 = pos >> 2;
+  uint32_t prev = 0;
+#pragma unroll
+  for (int m = 0; m <= OW; ++m) {
+    uint32_t cur = 0;
+    if (m < OW) {
+      const int left = (int)n - 4 * m;
+      const uint32_t mask = left >= 4 ? ~0u : left <= 0 ? 0u : ((1u << (8 * left)) - 1u);
+      cur = ow[m] & mask;
+    }
+    const uint32_t x = s8 ? __builtin_amdgcn_alignbit(cur, prev, 32u - s8) : cur;
+    if (4 * m < (int)((pos & 3u) + n)) atomicOr(&stg[w0 + m], x);
+    prev = cur;
+  }
+}
+
+// Copy a tile's staged bytes (tile-local offsets, after a 16-byte zero pad) to
+// out[goff, goff+n), clamped at out_cap.  Each lane builds one 16-byte output
+// chunk aligned to the global address from five aligned staging dwords and four
+// v_alignbyte (the tile's global offset is only known after its look-back, so the
+// staging cannot be pre-aligned); whole chunks go out as 16-byte stores, the two
+// edge chunks byte by byte.
+__device__ __forceinline__ void copy_out_shifted(const DecodeParams& p, const uint32_t* stg32,
+                                                 unsigned long long goff, uint32_t n, int tid) {
+  const uint32_t lb = (uint32_t)(goff & 15);
+  const unsigned long long a0 = goff - lb;
+  const unsigned long long end = min(goff + n, p.out_cap);
+  const uint32_t nz = (lb + n + 15u) >> 4;
+  for (uint32_t c = tid; c < nz; c += TB) {
+    const uint32_t sb = 16u * c + 16u - lb;  // staging byte of the chunk's first byte
+    const uint32_t wi = sb >> 2, sh = sb & 3u;
+    const uint32_t d0 = stg32[wi], d1 = stg32[wi + 1], d2 = stg32[wi + 2], d3 = stg32[wi + 3],
+                   d4 = stg32[wi + 4];
+    uint4 v;
+    v.x = __builtin_amdgcn_alignbyte(d1, d0, sh);
+    v.y = __builtin_amdgcn_alignbyte(d2, d1, sh);
+    v.z = __builtin_amdgcn_alignbyte(d3, d2, sh);
+    v.w = __builtin_amdgcn_alignbyte(d4, d3, sh);
+    const unsigned long long gs = a0 + 16ull * c;
+    if (gs >= goff && gs + 16 <= end) {
+      *(uint4*)(p.out + gs) = v;
+    } else {
+      const uint8_t* b = (const uint8_t*)&v;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const unsigned long long ga = gs + k;
+        if (ga >= goff && ga < end) p.out[ga] = b[k];
+      }
+    }
+  }
+}
+
+// The decode kernel.  One workgroup processes tiles of U*TB segments (thread t
+// owns segments tile*U*TB + u*TB + t, so every 16-byte load is coalesced) drawn
+// from an atomic ticket, software-pipelined across tiles:
+//
+//   iteration k:  decode/count tile k (its words were loaded during k-1)
+//                 -> scan, publish tile k's aggregate, draw ticket k+1
+//                 -> issue the loads of tile k+1
+//                 -> resolve tile k-1's prefix (its predecessors have had a whole
+//                    decode phase to publish), copy tile k-1 out
+//                 -> stage tile k's bytes at tile-local offsets
+//
+// Staging is double-buffered; each buffer is zeroed behind the copy-out that
+// drained it.  Three workgroup barriers per tile.
+//   SINGLE = true : single-symbol LUT, one decode pass, bytes held in registers
+//   SINGLE = false: multi-symbol LUT, count pass then emit pass.
+template <bool SINGLE, bool FB, int U>
 __global__ __launch_bounds__(TB) void gh_decode_kernel(const DecodeParams p) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint2* s_lut = (const uint2*)smem;
   const uint32_t* s_lut32 = (const uint32_t*)smem;
   uint32_t* s_fb = (uint32_t*)(smem + p.lut_bytes);
-  uint8_t* s_stage = smem + p.lut_bytes + FB_BYTES;
-  uint32_t* s_scr = (uint32_t*)(s_stage + p.stage_bytes);
-  // scratch: [0, 2*U*NWAVE) wave sums of two tiles, [32] ticket, [34..35] offset
+  uint8_t* s_stage0 = smem + p.lut_bytes + FB_BYTES;
+  uint32_t* s_scr = (uint32_t*)(s_stage0 + 2 * p.stage_bytes);
   uint32_t* s_ticket = s_scr + MAX_SUPER * NWAVE;
   unsigned long long* s_goff = (unsigned long long*)(s_scr + MAX_SUPER * NWAVE + 2);
 
@@ -445,8 +579,8 @@ __global__ __launch_bounds__(TB) void gh_decode_kernel(const DecodeParams p) {
     uint4* s = (uint4*)smem;
     for (uint32_t i = tid; i < p.lut_bytes / 16; i += TB) s[i] = g[i];
     for (uint32_t i = tid; i < (uint32_t)FB_WORDS; i += TB) s_fb[i] = p.fb[i];
-    uint4* st = (uint4*)s_stage;
-    for (uint32_t i = tid; i < p.stage_bytes / 16; i += TB) st[i] = make_uint4(0, 0, 0, 0);
+    uint4* st = (uint4*)s_stage0;
+    for (uint32_t i = tid; i < 2 * p.stage_bytes / 16; i += TB) st[i] = make_uint4(0, 0, 0, 0);
     if (tid == 0) *s_ticket = atomicAdd(p.ticket, 1u);
   }
   __syncthreads();
@@ -454,111 +588,131 @@ __global__ __launch_bounds__(TB) void gh_decode_kernel(const DecodeParams p) {
   const uint32_t kshift = 32u - p.kbits;
   STAMP_DECL
 
+  uint32_t cur = *s_ticket;
+  uint4 w[U];
+  uint32_t w4[U];
+  int start[U];
+  bool act[U];
+  if (cur < p.nsuper) load_tile<U>(p, cur, tid, w, w4, start, act);
+  bool seen_end = false;
+  uint32_t bad = 0;  // invalid bit pattern met (no-fallback build)
   bool have_prev = false;
-  uint32_t prev = 0, prev_total = 0, parity = 0;
-  uint32_t prev_bpos[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) prev_bpos[u] = 0;
+  uint32_t prev = 0, prev_total = 0;
+  uint32_t par = 0;                  // staging buffer of the current tile
+  uint32_t used0 = 0, used1 = 0;     // bytes last staged into buffer 0 / 1
 
   for (uint32_t iter = 0;; ++iter) {
     STAMP(9);
-    const uint32_t tile = *s_ticket;
-    const bool have_cur = tile < p.nsuper;
+    const bool have_cur = cur < p.nsuper;
     if (iter > p.nsuper + 1) {  // cannot happen; a guard so a logic error never hangs the GPU
       if (tid == 0) atomicOr(p.status, (unsigned)GH_ST_TIMEOUT);
       break;
     }
-    if (!have_cur && tid == 0 && tile == p.nsuper + gridDim.x - 1)
-      __hip_atomic_store(p.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!have_cur && !seen_end) {
+      seen_end = true;  // first out-of-range ticket: the last drawer resets the counter
+      if (tid == 0 && cur == p.nsuper + gridDim.x - 1)
+        __hip_atomic_store(p.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     if (!have_cur && !have_prev) break;
 
-    // ---- 1. new tile: load, count, scan, publish aggregate -------------------------
-    uint32_t cur_bpos[U];
-    uint32_t cur_total = 0;
-    uint32_t* sums = s_scr + parity * (U * NWAVE);
+    // ---- decode / count tile k ----------------------------------------------------
+    uint32_t cnt[U];
+    uint32_t ow[SINGLE ? U : 1][SINGLE ? OW : 1];
+    Win v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) cnt[u] = 0;
     if (have_cur) {
-      uint4 w[U];
-      uint32_t w4[U];
-      int start[U];
-      bool act[U];
-      load_tile<U>(p, tile, tid, w, w4, start, act);
-      STAMP(0);
-      Win v[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) v[u] = make_win(w[u], w4[u], start[u]);
-      uint32_t cnt[U];
-      count_segments<U>(v, start, act, cnt, s_lut32, s_fb, kshift, p);
-      STAMP(1);
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t incl = wave_incl_scan(cnt[u], lane);
-        if (lane == 63) sums[u * NWAVE + wid] = incl;
-        cur_bpos[u] = incl - cnt[u];
+      if constexpr (SINGLE) {
+        decode1_segments<FB, U>(v, start, act, ow, cnt, s_lut32, s_fb, kshift, p, bad);
+      } else {
+        count_segments<FB, U>(v, start, act, cnt, s_lut32, s_fb, kshift, p, bad);
       }
     }
-    __syncthreads();
+    STAMP(0);
+    uint32_t bpos[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t incl = wave_incl_scan(cnt[u], lane);
+      if (lane == 63) s_scr[u * NWAVE + wid] = incl;
+      bpos[u] = incl - cnt[u];
+    }
+    __syncthreads();  // B0: wave sums
+    STAMP(1);
+    uint32_t cur_total = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t before = cur_total;
+#pragma unroll
+      for (int q = 0; q < NWAVE; ++q) {
+        const uint32_t x = s_scr[u * NWAVE + q];
+        bpos[u] += (q < wid) ? x : 0u;
+        cur_total += x;
+      }
+      bpos[u] += before + 16u;  // 16-byte zero pad in front of the staged tile
+    }
+    if (tid == 0) {
+      if (have_cur) publish_aggregate(p, cur, cur_total);
+      *s_ticket = have_cur ? atomicAdd(p.ticket, 1u) : 0xFFFFFFFFu;
+    }
+    // clear this iteration's staging buffer (it held tile k-2, copied out at k-1)
+    {
+      uint4* st = (uint4*)(s_stage0 + par * p.stage_bytes);
+      const uint32_t nclr = ((par ? used1 : used0) + 16u + 15u) >> 4;
+      for (uint32_t i = tid; i < nclr; i += TB) st[i] = make_uint4(0, 0, 0, 0);
+    }
+    __syncthreads();  // B1: ticket, cleared buffer
     STAMP(2);
-    if (have_cur) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t before = cur_total;
-#pragma unroll
-        for (int q = 0; q < NWAVE; ++q) {
-          const uint32_t x = sums[u * NWAVE + q];
-          cur_bpos[u] += (q < wid) ? x : 0u;
-          cur_total += x;
-        }
-        cur_bpos[u] += before;
+    const uint32_t next = *s_ticket;
+    // the words of tile k are still needed by the emit pass (two-pass path)
+    uint4 wn[U];
+    uint32_t w4n[U];
+    int startn[U];
+    bool actn[U];
+    if (next < p.nsuper) load_tile<U>(p, next, tid, wn, w4n, startn, actn);
+    if (have_prev && wid == 0) {
+      const unsigned long long ex = ABLATE(1) ? 0ull : resolve_prefix(p, prev, prev_total, lane);
+      if (lane == 0) {
+        *s_goff = ex;
+        if (prev == p.nsuper - 1) *p.total = ex + prev_total;
       }
-      if (tid == 0) publish_aggregate(p, tile, cur_total);
     }
-
-    // ---- 2. previous tile: resolve prefix, emit, store ---------------------------------
-    if (have_prev) {
-      uint4 w[U];
-      uint32_t w4[U];
-      int start[U];
-      bool act[U];
-      load_tile<U>(p, prev, tid, w, w4, start, act);  // L2-resident re-read
-      if (wid == 0) {
-        const unsigned long long ex = resolve_prefix(p, prev, prev_total, lane);
-        if (lane == 0) {
-          *s_goff = ex;
-          if (prev == p.nsuper - 1) *p.total = ex + prev_total;
-        }
-      }
-      STAMP(3);
-      __syncthreads();
-      STAMP(4);
-      if (tid == 0)  // next tile, drawn before the emit; none after the first out-of-range one
-        *s_ticket = have_cur ? atomicAdd(p.ticket, 1u) : 0xFFFFFFFFu;
-      const unsigned long long goff = *s_goff;
-      const uint32_t lb = (uint32_t)(goff & 15);
-      Win v[U];
-      uint32_t bpos[U];
+    STAMP(3);
+    __syncthreads();  // B2: prefix of tile k-1
+    STAMP(4);
+    if (have_prev && !ABLATE(2))
+      copy_out_shifted(p, (const uint32_t*)(s_stage0 + (par ^ 1u) * p.stage_bytes), *s_goff,
+                       prev_total, tid);
+    STAMP(5);
+    if (have_cur && !ABLATE(4)) {
+      uint32_t* stg = (uint32_t*)(s_stage0 + par * p.stage_bytes);
+      if constexpr (SINGLE) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        v[u] = make_win(w[u], w4[u], start[u]);
-        bpos[u] = prev_bpos[u] + lb;
+        for (int u = 0; u < U; ++u)
+          if (cnt[u]) stage_bytes(stg, ow[u], cnt[u], bpos[u]);
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = make_win(w[u], w4[u], start[u]);
+        emit_segments<FB, U>(v, start, act, bpos, s_lut, s_fb, kshift, p, stg);
       }
-      emit_segments<U>(v, start, act, bpos, s_lut, s_fb, kshift, p, (uint32_t*)s_stage);
-      STAMP(5);
-      __syncthreads();
-      STAMP(6);
-      copy_out(p, (uint4*)s_stage, goff, prev_total, tid);
-      STAMP(7);
-    } else {
-      if (tid == 0) *s_ticket = have_cur ? atomicAdd(p.ticket, 1u) : 0xFFFFFFFFu;
     }
-    __syncthreads();
-    STAMP(8);
+    STAMP(6);
     have_prev = have_cur;
-    prev = tile;
+    prev = cur;
     prev_total = cur_total;
+    if (par) used1 = have_cur ? cur_total : 0u; else used0 = have_cur ? cur_total : 0u;
+    par ^= 1u;
+    cur = next;
 #pragma unroll
-    for (int u = 0; u < U; ++u) prev_bpos[u] = cur_bpos[u];
-    parity ^= 1u;
+    for (int u = 0; u < U; ++u) {
+      w[u] = wn[u];
+      w4[u] = w4n[u];
+      start[u] = startn[u];
+      act[u] = actn[u];
+    }
   }
+  if (!FB && __any(bad != 0) && lane == 0) atomicOr(p.status, (unsigned)GH_ST_BADCODE);
   STAMP_FLUSH;
 }
 
@@ -567,7 +721,10 @@ __global__ __launch_bounds__(TB) void gh_decode_kernel(const DecodeParams p) {
 // ============================================================================
 struct Tables {
   uint32_t K = 0;
-  std::vector<uint2> lut;            // 2^K entries
+  bool single = false;               // single-symbol single-pass path (u32 LUT)
+  bool needs_fb = true;              // some codeword is longer than the LUT width K
+  std::vector<uint2> lut;            // 2^K multi-symbol entries
+  std::vector<uint32_t> lut1;        // 2^K single-symbol entries
   uint32_t fb[FB_WORDS] = {};
   uint32_t fb_lo = 1, fb_hi = 1;
   uint32_t maxsyms_seg = 128;
@@ -625,14 +782,44 @@ static uint32_t choose_k(const Canon& c) {
   return bestk;
 }
 
-static int build_tables(const Canon& c, Tables& t, int force_k) {
-  if (c.nsyms == 0) return fail(GH_E_TABLE, "empty code");
-  t.K = force_k > 0 ? (uint32_t)std::clamp(force_k, 1, 12) : choose_k(c);
-  t.lut.assign(1u << t.K, make_uint2(0, 0));
-  for (uint32_t i = 0; i < (1u << t.K); ++i) {
+// Expected symbols per lookup of the multi-symbol table at width K.
+static double multi_gain(const Canon& c, uint32_t K) {
+  double syms = 0;
+  for (uint32_t i = 0; i < (1u << K); ++i) {
     uint32_t s;
-    const uint32_t m = lut_meta_for(c, i, t.K, &s);
-    t.lut[i] = make_uint2(s, m);
+    const uint32_t n = (lut_meta_for(c, i, K, &s) >> 16) & 7u;
+    syms += n ? n : 1;
+  }
+  return syms / (double)(1u << K);
+}
+
+static int build_tables(const Canon& c, Tables& t, int force_k, int force_path) {
+  if (c.nsyms == 0) return fail(GH_E_TABLE, "empty code");
+  // Single-pass single-symbol path when every segment fits 32 symbols (minlen >= 4)
+  // and 12-bit multi-symbol lookups would average < 1.5 symbols.
+  t.single = (force_path == 1) || (force_path != 2 && c.minlen >= 4 && multi_gain(c, 12) < 1.5);
+  if (c.minlen < 4) t.single = false;
+  if (t.single) {
+    t.K = force_k > 0 ? (uint32_t)std::clamp(force_k, 1, 12) : std::min<uint32_t>(c.maxlen, 12);
+    t.lut1.assign(1u << t.K, 0u);
+    for (uint32_t i = 0; i < (1u << t.K); ++i) {
+      uint32_t fi = 0;
+      const uint32_t l = canon_decode16(c, (i << (32 - t.K)) >> 16, &fi);
+      if (l == 0 || l > t.K) continue;  // fallback entry (b = 0)
+      t.lut1[i] = ((32u - l) & 31u) | (l << 8) | ((uint32_t)c.sym[fi] << 24);
+    }
+    t.lut.clear();
+    if (t.lut1.size() < 4) t.lut1.resize(4, 0u);  // LDS copy moves 16-byte chunks
+  } else {
+    t.K = force_k > 0 ? (uint32_t)std::clamp(force_k, 1, 12) : choose_k(c);
+    t.lut.assign(1u << t.K, make_uint2(0, 0));
+    for (uint32_t i = 0; i < (1u << t.K); ++i) {
+      uint32_t s;
+      const uint32_t m = lut_meta_for(c, i, t.K, &s);
+      t.lut[i] = make_uint2(s, m);
+    }
+    if (t.lut.size() < 2) t.lut.resize(2, make_uint2(0, 0));
+    t.lut1.clear();
   }
   // fallback: running limits so empty lengths never match
   uint32_t run = 0;
@@ -648,6 +835,7 @@ static int build_tables(const Canon& c, Tables& t, int force_k) {
   t.fb_lo = std::max<uint32_t>(t.fb_lo, c.minlen);
   t.fb_hi = std::max<uint32_t>(c.maxlen, t.fb_lo);
   t.maxsyms_seg = (128 + c.minlen - 1) / c.minlen;
+  t.needs_fb = c.maxlen > t.K;
   return GH_OK;
 }
 
@@ -662,12 +850,25 @@ using namespace gh;
       return fail(GH_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));   \
   } while (0)
 
-static const void* kernel_for(int uv) {
+static void** args_of(DecodeParams& p) {
+  static thread_local void* a[1];
+  a[0] = &p;
+  return a;
+}
+
+template <bool SINGLE, bool FB>
+static const void* kernel_for_u(int uv) {
   switch (uv) {
-    case 4: return (const void*)gh_decode_kernel<4>;
-    case 2: return (const void*)gh_decode_kernel<2>;
-    default: return (const void*)gh_decode_kernel<1>;
+    case 4: return (const void*)gh_decode_kernel<SINGLE, FB, 4>;
+    case 2: return (const void*)gh_decode_kernel<SINGLE, FB, 2>;
+    default: return (const void*)gh_decode_kernel<SINGLE, FB, 1>;
   }
+}
+
+// The no-fallback variants apply when every codeword fits the LUT width.
+static const void* kernel_for(bool single, bool fb, int uv) {
+  if (single) return fb ? kernel_for_u<true, true>(uv) : kernel_for_u<true, false>(uv);
+  return fb ? kernel_for_u<false, true>(uv) : kernel_for_u<false, false>(uv);
 }
 
 struct gh_ctx {
@@ -742,9 +943,11 @@ extern "C" int gh_ctx_create(int device, gh_ctx** out) {
   GH_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   GH_HIP(hipMalloc(&c->d_misc, 64));
   GH_HIP(hipMemset(c->d_misc, 0, 64));
-  for (int sv : {1, 2, 4})
-    (void)hipFuncSetAttribute(kernel_for(sv), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
+  for (bool sg : {false, true})
+    for (bool fbv : {false, true})
+      for (int sv : {1, 2, 4})
+        (void)hipFuncSetAttribute(kernel_for(sg, fbv, sv),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   (void)hipGetLastError();
   *out = c;
   return GH_OK;
@@ -781,7 +984,8 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
   c->n_total = s->n;
   if (c->nseg > 0) {
     const char* envk = getenv("GH_LUT_BITS");
-    rc = build_tables(c->canon, c->tables, envk ? atoi(envk) : 0);
+    const char* envp = getenv("GH_PATH");
+    rc = build_tables(c->canon, c->tables, envk ? atoi(envk) : 0, envp ? atoi(envp) : 0);
     if (rc) return rc;
   }
   const uint64_t bound = c->nseg * (uint64_t)std::max<uint32_t>(c->tables.maxsyms_seg, 1);
@@ -794,9 +998,13 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
   c->ntiles = 0;
   c->grid = 0;
   if (c->nseg > 0) {
-    const size_t lut_bytes = c->tables.lut.size() * sizeof(uint2);
+    const size_t lut_bytes = c->tables.single ? c->tables.lut1.size() * sizeof(uint32_t)
+                                              : c->tables.lut.size() * sizeof(uint2);
+    const void* lut_src = c->tables.single ? (const void*)c->tables.lut1.data()
+                                           : (const void*)c->tables.lut.data();
     GH_HIP(hipMalloc(&c->d_lut, std::max<size_t>(lut_bytes, 16)));
-    GH_HIP(hipMemcpy(c->d_lut, c->tables.lut.data(), lut_bytes, hipMemcpyHostToDevice));
+    GH_HIP(hipMemset(c->d_lut, 0, std::max<size_t>(lut_bytes, 16)));
+    GH_HIP(hipMemcpy(c->d_lut, lut_src, lut_bytes, hipMemcpyHostToDevice));
     GH_HIP(hipMalloc(&c->d_fb, sizeof(c->tables.fb)));
     GH_HIP(hipMemcpy(c->d_fb, c->tables.fb, sizeof(c->tables.fb), hipMemcpyHostToDevice));
     // Segments per thread (ILP): as many as keep the tile's staging <= 32 KiB.
@@ -804,17 +1012,22 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
     int uv = envu ? atoi(envu) : 0;
     if (uv != 1 && uv != 2 && uv != 4) {
       const uint32_t per = TB * c->tables.maxsyms_seg;
-      uv = (4 * per <= 32768) ? 4 : (2 * per <= 32768) ? 2 : 1;
+      uv = c->tables.single ? 2 : (4 * per <= 16384) ? 4 : (2 * per <= 16384) ? 2 : 1;
     }
-    c->super = (uint32_t)uv;
-    c->stage_bytes = (uint32_t)(((uint64_t)uv * TB * c->tables.maxsyms_seg + 32 + 15) & ~15ull);
-    c->lds = lut_bytes + FB_BYTES + c->stage_bytes + SCRATCH_BYTES;
-    int per_cu = 0;
-    GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_for(uv), TB, c->lds));
-    if (per_cu >= 1) {
-      const uint64_t grid = (uint64_t)per_cu * c->num_cu;
-      c->ntiles = (uint32_t)ceil_div(c->nseg, (uint64_t)uv * TB);
-      c->grid = (uint32_t)std::min<uint64_t>(c->ntiles, grid);
+    for (;; uv >>= 1) {  // fall back to a narrower ILP width if the kernel does not fit
+      c->super = (uint32_t)uv;
+      c->stage_bytes = (uint32_t)(((uint64_t)uv * TB * c->tables.maxsyms_seg + 64 + 15) & ~15ull);
+      c->lds = lut_bytes + FB_BYTES + 2 * c->stage_bytes + SCRATCH_BYTES;
+      int per_cu = 0;
+      GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+          &per_cu, kernel_for(c->tables.single, c->tables.needs_fb, uv), TB, c->lds));
+      if (per_cu >= 1) {
+        const uint64_t grid = (uint64_t)per_cu * c->num_cu;
+        c->ntiles = (uint32_t)ceil_div(c->nseg, (uint64_t)uv * TB);
+        c->grid = (uint32_t)std::min<uint64_t>(c->ntiles, grid);
+        break;
+      }
+      if (uv == 1) break;
     }
     if (c->grid == 0) return fail(GH_E_HIP, "decode kernel does not fit on a CU");
 #ifdef GH_STAMPS
@@ -938,11 +1151,16 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
   p.nsuper = c->ntiles;
   p.kbits = c->tables.K;
   p.epoch = c->epoch;
-  p.lut_bytes = (uint32_t)(c->tables.lut.size() * sizeof(uint2));
+  p.lut_bytes = (uint32_t)(c->tables.single ? c->tables.lut1.size() * sizeof(uint32_t)
+                                            : c->tables.lut.size() * sizeof(uint2));
   p.stage_bytes = c->stage_bytes;
   p.fb_lo = c->tables.fb_lo;
   p.fb_hi = c->tables.fb_hi;
   p.stamps = c->d_stamps;
+  {
+    const char* ab = getenv("GH_ABLATE");
+    p.ablate = ab ? (unsigned)atoi(ab) : 0u;
+  }
   std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
   if (timed) {
     if (!c->pool.empty()) {
@@ -954,11 +1172,9 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     }
     GH_HIP(hipEventRecord(ev.first, st));
   }
-  switch (c->super) {
-    case 4: hipLaunchKernelGGL(gh_decode_kernel<4>, dim3(c->grid), dim3(TB), c->lds, st, p); break;
-    case 2: hipLaunchKernelGGL(gh_decode_kernel<2>, dim3(c->grid), dim3(TB), c->lds, st, p); break;
-    default: hipLaunchKernelGGL(gh_decode_kernel<1>, dim3(c->grid), dim3(TB), c->lds, st, p); break;
-  }
+  GH_HIP(hipLaunchKernel(kernel_for(c->tables.single, c->tables.needs_fb, (int)c->super),
+                         dim3(c->grid), dim3(TB),
+                         args_of(p), c->lds, st));
   GH_HIP(hipGetLastError());
   if (timed) {
     GH_HIP(hipEventRecord(ev.second, st));

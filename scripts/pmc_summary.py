@@ -4,13 +4,13 @@ root = sys.argv[1]
 vals = collections.defaultdict(list)
 for f in glob.glob(os.path.join(root, "*", "**", "*counter_collection.csv"), recursive=True):
     for row in csv.DictReader(open(f)):
-        if "gh_decode_kernel" not in row.get("Kernel_Name", ""):
+        if "gh_decode" not in row.get("Kernel_Name", ""):
             continue
         vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
 dur = []
 for f in glob.glob(os.path.join(root, "*", "**", "*kernel_trace.csv"), recursive=True):
     for row in csv.DictReader(open(f)):
-        if "gh_decode_kernel" in row.get("Kernel_Name", ""):
+        if "gh_decode" in row.get("Kernel_Name", ""):
             dur.append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e3)
 out = {k: sum(v) / len(v) for k, v in vals.items()}
 for k in sorted(out):

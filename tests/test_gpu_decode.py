@@ -151,3 +151,22 @@ def test_config_1GB_bitexact(gpu, cfg):
     img = gpu.encode(data)
     out = gpu.decode(img)
     assert np.array_equal(out, data)
+
+
+@pytest.mark.parametrize("path", ["1", "2"])
+@pytest.mark.parametrize("u", ["1", "2", "4"])
+def test_decode_paths_and_ilp(gpu, orc, path, u, monkeypatch):
+    """Both decode paths (1 = single-pass single-symbol, 2 = count + emit with
+    multi-symbol lookups) and every ILP width give identical bytes."""
+    monkeypatch.setenv("GH_PATH", path)
+    monkeypatch.setenv("GH_U", u)
+    cases = [gpu.generate(21, 0.1, 300_001), gpu.generate(22, 0.0, 77_777)]
+    x = np.tile(np.arange(256, dtype=np.uint8), 300)
+    np.random.default_rng(2).shuffle(x)
+    cases.append(x)
+    counts = [max(1, int(2 ** (15 - 0.35 * i))) for i in range(40)]
+    g = np.repeat(np.arange(40, dtype=np.uint8) + 60, counts)
+    np.random.default_rng(4).shuffle(g)
+    cases.append(g)  # minlen >= 4 with long codes -> fallback inside path 1
+    for d in cases:
+        _roundtrip(gpu, orc, d)
