@@ -1238,6 +1238,17 @@ extern "C" int gh_ctx_output(gh_ctx* c, void** d_out, uint64_t* cap) {
   return GH_OK;
 }
 
+extern "C" int gh_ctx_copy_output(gh_ctx* c, uint64_t off, void* dst, uint64_t nbytes,
+                                  void* hip_stream) {
+  if (!c || (nbytes && !dst)) return fail(GH_E_ARG, "null argument");
+  if (off + nbytes > c->out_cap) return fail(GH_E_ARG, "copy beyond the output capacity");
+  if (!nbytes) return GH_OK;
+  hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
+  GH_HIP(hipSetDevice(c->device));
+  GH_HIP(hipMemcpyAsync(dst, c->d_out + off, nbytes, hipMemcpyDefault, st));
+  return GH_OK;
+}
+
 extern "C" int gh_decode(const gh_stream* s, uint8_t* out, uint64_t out_len, const gh_opts* o,
                          gh_report* rep) {
   if (!s || (s->n && !out)) return fail(GH_E_ARG, "null argument");

@@ -43,7 +43,7 @@ EXPORTED = (
     "gh_stream_parse", "gh_stream_validate", "gh_encode_plan_make", "gh_encode_write",
     "gh_package_merge", "gh_generate", "gh_ctx_create", "gh_ctx_destroy", "gh_ctx_load",
     "gh_ctx_load_device", "gh_ctx_decode", "gh_ctx_report", "gh_ctx_download",
-    "gh_ctx_output", "gh_ctx_reset_timing", "gh_decode", "gh_plan_shards",
+    "gh_ctx_output", "gh_ctx_copy_output", "gh_ctx_reset_timing", "gh_decode", "gh_plan_shards",
     "gh_device_count", "gh_version", "gh_last_error",
 )
 
@@ -114,6 +114,7 @@ def lib() -> ctypes.CDLL:
             "gh_ctx_report": ([P, P, ctypes.POINTER(gh_report)], I),
             "gh_ctx_download": ([P, U64, P, U64], I),
             "gh_ctx_output": ([P, ctypes.POINTER(P), ctypes.POINTER(U64)], I),
+            "gh_ctx_copy_output": ([P, U64, P, U64, P], I),
             "gh_ctx_reset_timing": ([P], I),
             "gh_decode": ([ctypes.POINTER(gh_stream), P, U64, ctypes.POINTER(gh_opts),
                            ctypes.POINTER(gh_report)], I),
@@ -270,6 +271,11 @@ class Decoder:
         out = np.empty(nbytes, dtype=np.uint8)
         _check(lib().gh_ctx_download(self._h, offset, _ptr(out), nbytes))
         return out
+
+    def copy_output(self, dst_ptr: int, nbytes: int, offset: int = 0, hip_stream: int = 0) -> None:
+        """Async copy of shard output bytes to a device/host address (e.g. a torch tensor)."""
+        _check(lib().gh_ctx_copy_output(self._h, offset, ctypes.c_void_p(dst_ptr), nbytes,
+                                        ctypes.c_void_p(hip_stream or None)))
 
     def output(self):
         p = ctypes.c_void_p()

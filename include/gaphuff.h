@@ -158,6 +158,10 @@ int gh_ctx_report(gh_ctx* ctx, void* hip_stream, gh_report* rep);
 int gh_ctx_download(gh_ctx* ctx, uint64_t byte_offset, uint8_t* dst, uint64_t nbytes);
 /* Device pointer of the shard output (for RCCL gathers / torch interop). */
 int gh_ctx_output(gh_ctx* ctx, void** d_out, uint64_t* cap);
+/* Asynchronously copy nbytes of the shard output (from byte_offset) to `dst`
+ * (device or host memory) on `hip_stream` (NULL = the context's stream). */
+int gh_ctx_copy_output(gh_ctx* ctx, uint64_t byte_offset, void* dst, uint64_t nbytes,
+                       void* hip_stream);
 /* Reset the accumulated kernel timing. */
 int gh_ctx_reset_timing(gh_ctx* ctx);
 

@@ -170,3 +170,30 @@ def test_decode_paths_and_ilp(gpu, orc, path, u, monkeypatch):
     cases.append(g)  # minlen >= 4 with long codes -> fallback inside path 1
     for d in cases:
         _roundtrip(gpu, orc, d)
+
+
+@pytest.mark.gpu
+def test_bench_contract_small(gpu):
+    """bench.py prints one JSON line with the contract keys (small size, no CPU leg)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "3", "--warmup", "1",
+                        "--size", "3000000", "--cpu-sample", "0"], capture_output=True, text=True,
+                       timeout=300, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1
+    j = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config", "roofline"):
+        assert k in j
+    assert j["bitexact"] is True and j["value"] > 0
+    assert 0 < j["roofline"]["frac"] < 1
+
+
+@pytest.mark.gpu
+def test_graft_smoke(gpu):
+    import __graft_entry__
+    __graft_entry__.smoke()
