@@ -119,7 +119,7 @@ def main() -> int:
     ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
     ap.add_argument("--size", type=int, default=0, help="bytes per GPU (overrides workload)")
     ap.add_argument("--seed", type=int, default=375)
-    ap.add_argument("--cpu-sample", type=int, default=5 * 10**7,
+    ap.add_argument("--cpu-sample", type=int, default=10**8,
                     help="bytes decoded by the CPU baseline (0 = skip)")
     ap.add_argument("--threads", type=int, default=16, help="host threads for generate/encode")
     args = ap.parse_args()

@@ -45,7 +45,7 @@ constexpr int NWAVE = TB / 64;
 constexpr int FB_WORDS = 3 * 17 + 64;    // limit16/base16/first + 256 symbol bytes
 constexpr int FB_BYTES = ((4 * FB_WORDS) + 15) & ~15;
 constexpr int MAX_SUPER = 8;             // sub-tiles per super-tile (template values 1,2,4,8)
-constexpr int SCRATCH_BYTES = 4 * (MAX_SUPER * NWAVE + 8);
+constexpr int SCRATCH_BYTES = 4 * (MAX_SUPER * NWAVE + 8) + 16 * NWAVE + 16;
 constexpr uint32_t EPOCH_MAX = (1u << 24) - 1;
 constexpr uint32_t SPIN_LIMIT = 1u << 18;
 
@@ -71,6 +71,7 @@ struct DecodeParams {
   unsigned int fb_lo, fb_hi;     // fallback length range
   unsigned long long* stamps;    // diagnostic build only (GH_STAMPS): per-block phase cycles
   unsigned int ablate;           // diagnostic build only: 1 no resolve, 2 no copy-out, 4 no stage
+  unsigned int sched;            // 0: tiles from the atomic ticket; 1: static round robin
 };
 #ifdef GH_STAMPS
 #define ABLATE(bit) (p.ablate & (bit))
@@ -325,12 +326,12 @@ __device__ __forceinline__ void publish_aggregate(const DecodeParams& p, uint32_
                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ unsigned long long resolve_prefix(const DecodeParams& p, uint32_t tile,
-                                             unsigned long long total, int lane) {
+// Slow path of the look-back (one wave): rounds of 256 granules from `base` down,
+// adding aggregates until an inclusive prefix; re-fetches while a predecessor
+// has not published.  Returns the exclusive prefix of `tile` (does not publish).
+__device__ unsigned long long resolve_slow(const DecodeParams& p, long long base,
+                                           unsigned long long excl, int lane) {
   constexpr unsigned long long VMASK = (1ull << 38) - 1;
-  if (tile == 0) return 0;
-  unsigned long long excl = 0;
-  long long base = (long long)tile - 1;
   uint32_t spins = 0;
   for (;;) {
     unsigned long long g[4];
@@ -372,35 +373,93 @@ __device__ unsigned long long resolve_prefix(const DecodeParams& p, uint32_t til
     if (fp < 256) break;
     base -= 256;
   }
-  if (lane == 0)
-    __hip_atomic_store(&p.granules[tile], granule(p.epoch, 2, excl + total), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
   return excl;
 }
 
+// Fast path of the look-back, spread over the whole workgroup: wave w fetches the
+// granules at distances [256w, 256w+256) before the tile (issued early, so the
+// fabric round trip overlaps the staging), then summarises them: nearest
+// inclusive prefix, whether everything up to it has published, and the sum.
+struct LbSummary {
+  unsigned long long sum;
+  uint32_t fp;  // local distance of the nearest inclusive prefix (256: none)
+  uint32_t ok;
+};
+
+__device__ __forceinline__ void lookback_issue(const DecodeParams& p, uint32_t tile, int wid,
+                                               int lane, unsigned long long (&g)[4]) {
+  // unconditional loads (clamped index): a skipped load would make the compiler
+  // wait for every later load before the summary
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const long long pi = (long long)tile - 1 - 256 * wid - 64 * j - lane;
+    g[j] = __hip_atomic_load(&p.granules[pi < 0 ? 0 : pi], __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__device__ __forceinline__ void lookback_summarise(const DecodeParams& p, uint32_t tile, int wid,
+                                                   int lane, const unsigned long long (&g)[4],
+                                                   LbSummary* out) {
+  constexpr unsigned long long VMASK = (1ull << 38) - 1;
+  const long long base = (long long)tile - 1 - 256 * wid;
+  uint32_t st[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    st[j] = (base - 64 * j - lane < 0) ? 2u
+            : ((uint32_t)(g[j] >> 40) == p.epoch) ? (uint32_t)((g[j] >> 38) & 3u) : 0u;
+  int fp = 256;
+#pragma unroll
+  for (int j = 3; j >= 0; --j) {
+    const unsigned long long pm = __ballot(st[j] == 2);
+    if (pm) fp = 64 * j + __builtin_ctzll(pm);
+  }
+  bool ok = true;
+  unsigned long long v = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int d = 64 * j + lane;
+    ok &= (d > fp) || (st[j] != 0);
+    if (d <= fp && base - d >= 0) v += g[j] & VMASK;
+  }
+  const bool all_ok = __all(ok);
+  v = wave_sum_u64(v);
+  if (lane == 0) *out = LbSummary{v, (uint32_t)fp, all_ok ? 1u : 0u};
+}
+
 // Load the U segments of a tile owned by this thread (16-byte loads, coalesced).
+// The gap word is kept raw: extracting the nibble here would make the compiler
+// wait for the loads right away; tile_starts() does it when the tile is decoded.
 template <int U>
 __device__ __forceinline__ void load_tile(const DecodeParams& p, uint32_t tile, int tid,
-                                          uint4 (&w)[U], uint32_t (&w4)[U], int (&start)[U],
+                                          uint4 (&w)[U], uint32_t (&w4)[U], uint32_t (&gw)[U],
                                           bool (&act)[U]) {
+  // Loads are unconditional (clamped to the last tile / segment): a load skipped
+  // by a branch would make the compiler's wait counting fall back to vmcnt(0).
+  const uint32_t t = min(tile, p.nsuper - 1);
+  const unsigned long long seg0 = (unsigned long long)t * (U * TB) + tid;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const unsigned long long seg = seg0 + (unsigned long long)u * TB;
+    act[u] = tile < p.nsuper && seg < p.nseg;
+    const unsigned long long sc = min(seg, p.nseg - 1);
+    w[u] = *(const uint4*)(p.payload + 4 * sc);
+    w4[u] = p.payload[4 * sc + 4];
+    gw[u] = p.gaps[((unsigned long long)p.gap_nib0 + (sc ? sc - 1 : 0)) >> 3];
+  }
+}
+
+// Start bit of each segment of the tile (its gap nibble, or first_start for the
+// shard's first segment).
+template <int U>
+__device__ __forceinline__ void tile_starts(const DecodeParams& p, uint32_t tile, int tid,
+                                            const uint32_t (&gw)[U], int (&start)[U]) {
   const unsigned long long seg0 = (unsigned long long)tile * (U * TB) + tid;
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const unsigned long long seg = seg0 + (unsigned long long)u * TB;
-    act[u] = seg < p.nseg;
-    start[u] = 0;
-    w[u] = make_uint4(0, 0, 0, 0);
-    w4[u] = 0;
-    if (act[u]) {
-      w[u] = *(const uint4*)(p.payload + 4 * seg);
-      w4[u] = p.payload[4 * seg + 4];
-      if (seg == 0) {
-        start[u] = (int)p.first_start;
-      } else {
-        const unsigned long long nib = (unsigned long long)p.gap_nib0 + seg - 1;
-        start[u] = (int)((p.gaps[nib >> 3] >> (4 * (nib & 7))) & 15u);
-      }
-    }
+    const uint32_t nib = (uint32_t)(p.gap_nib0 + seg - 1) & 7u;
+    start[u] = seg == 0 ? (int)p.first_start : (int)((gw[u] >> (4 * nib)) & 15u);
   }
 }
 
@@ -487,6 +546,91 @@ __device__ __forceinline__ void decode1_segments(Win (&v)[U], const int (&start)
   }
 }
 
+// ---------------------------------------------------------------------------
+// Grouped single-symbol path (complete codes, every codeword <= K bits, minlen
+// >= 4 — e.g. redundancy 0.1).  Same static output positions as above, but the
+// 160-bit window is shifted only once per group of G codewords (G*maxlen <= 31):
+// inside a group the next codeword sits at bit p of d0:d1 and is extracted with
+// one v_alignbit by q = 32 - p (q is decremented by the code length; the group's
+// first lookup reads d0 directly, p = 0).  LUT entries are 8 bytes
+// {len, sym << 24}, so q stays exact and doubles as the liveness test: a
+// codeword is kept iff it starts before bit 128, i.e. q > T with T = F + 32 - L
+// (F = bits flushed so far, L = 128 - start).  Dead lanes insert a zero byte, so
+// the bytes past cnt are zero and staging needs no masks.  No invalid-pattern
+// check: a complete prefix code decodes every bit pattern.
+// ---------------------------------------------------------------------------
+template <int U, int G>
+__device__ __forceinline__ void decode1g(Win (&v)[U], const int (&start)[U], const bool (&act)[U],
+                                         uint32_t (&ow)[U][OW], uint32_t (&cnt)[U],
+                                         const uint8_t* s_lut8, uint32_t ksh8) {
+  constexpr int S = 4 * OW;
+  constexpr int NG = (S + G - 1) / G;
+  uint32_t q[U];
+  int T[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    q[u] = 32;
+    T[u] = act[u] ? start[u] - 96 : 0x7FFFFFFF;  // 32 - L, L = 128 - start
+    cnt[u] = 0;
+#pragma unroll
+    for (int k = 0; k < OW; ++k) ow[u][k] = 0;
+  }
+#pragma unroll
+  for (int gi = 0; gi < NG; ++gi) {
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      const int pos = gi * G + j;
+      if (pos < S) {
+        uint2 e[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint32_t w = j == 0 ? v[u].d0 : __builtin_amdgcn_alignbit(v[u].d0, v[u].d1, q[u]);
+          e[u] = *(const uint2*)(s_lut8 + ((w >> ksh8) & ~7u));
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const bool live = (int)q[u] > T[u];
+          cnt[u] += live ? 1u : 0u;
+          const uint32_t sb = live ? e[u].y : 0u;
+          ow[u][pos >> 2] = __builtin_amdgcn_perm(sb, ow[u][pos >> 2], perm_sel(pos & 3));
+          q[u] -= e[u].x;
+        }
+      }
+    }
+    // flush: shift the window left by p = 32 - q (1 <= p <= 31)
+    bool more = false;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      v[u].d0 = __builtin_amdgcn_alignbit(v[u].d0, v[u].d1, q[u]);
+      v[u].d1 = __builtin_amdgcn_alignbit(v[u].d1, v[u].d2, q[u]);
+      v[u].d2 = __builtin_amdgcn_alignbit(v[u].d2, v[u].d3, q[u]);
+      v[u].d3 = __builtin_amdgcn_alignbit(v[u].d3, v[u].d4, q[u]);
+      v[u].d4 = __builtin_amdgcn_alignbit(v[u].d4, 0u, q[u]);
+      T[u] += 32 - (int)q[u];
+      q[u] = 32;
+      more |= 32 > T[u];
+    }
+    if (gi + 1 < NG && !__any(more)) break;
+  }
+}
+
+// Stage a segment's bytes whose tail (past n) is already zero: nine funnel-shifted
+// words ORed at byte position pos.  For pos % 4 == 0 the funnel by 0 yields the
+// previous word, so the words land one slot lower (slot -1 gets a harmless 0).
+__device__ __forceinline__ void stage_bytes_z(uint32_t* stg, const uint32_t (&ow)[OW],
+                                              uint32_t pos) {
+  const uint32_t s8 = 8u * (pos & 3u);
+  const uint32_t sh = (32u - s8) & 31u;
+  uint32_t* base = stg + (pos >> 2) - (s8 == 0 ? 1 : 0);
+  uint32_t prev = 0;
+#pragma unroll
+  for (int m = 0; m <= OW; ++m) {
+    const uint32_t cur = m < OW ? ow[m] : 0u;
+    atomicOr(base + m, __builtin_amdgcn_alignbit(cur, prev, sh));
+    prev = cur;
+  }
+}
+
 // OR a segment's n output bytes (held in registers) into the staging buffer at
 // byte position pos.
 __device__ __forceinline__ void stage_bytes(uint32_t* stg, const uint32_t (&ow)[OW], uint32_t n,
@@ -559,8 +703,9 @@ __device__ __forceinline__ void copy_out_shifted(const DecodeParams& p, const ui
 // drained it.  Three workgroup barriers per tile.
 //   SINGLE = true : single-symbol LUT, one decode pass, bytes held in registers
 //   SINGLE = false: multi-symbol LUT, count pass then emit pass.
-template <bool SINGLE, bool FB, int U>
+template <bool SINGLE, bool FB, int U, int G>
 __global__ __launch_bounds__(TB) void gh_decode_kernel(const DecodeParams p) {
+  static_assert(G == 0 || (SINGLE && !FB), "grouped path: single-symbol, no fallback");
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint2* s_lut = (const uint2*)smem;
   const uint32_t* s_lut32 = (const uint32_t*)smem;
@@ -569,6 +714,7 @@ __global__ __launch_bounds__(TB) void gh_decode_kernel(const DecodeParams p) {
   uint32_t* s_scr = (uint32_t*)(s_stage0 + 2 * p.stage_bytes);
   uint32_t* s_ticket = s_scr + MAX_SUPER * NWAVE;
   unsigned long long* s_goff = (unsigned long long*)(s_scr + MAX_SUPER * NWAVE + 2);
+  LbSummary* s_lb = (LbSummary*)(s_goff + 1);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -581,7 +727,26 @@ __global__ __launch_bounds__(TB) void gh_decode_kernel(const DecodeParams p) {
     for (uint32_t i = tid; i < (uint32_t)FB_WORDS; i += TB) s_fb[i] = p.fb[i];
     uint4* st = (uint4*)s_stage0;
     for (uint32_t i = tid; i < 2 * p.stage_bytes / 16; i += TB) st[i] = make_uint4(0, 0, 0, 0);
-    if (tid == 0) *s_ticket = atomicAdd(p.ticket, 1u);
+  }
+  // thread 0: ticket drawn for the iteration after next.  `pend` is only ever
+  // written by the atomic (a plain write would have to wait for it); whether a
+  // draw is outstanding is kept apart in `pend_ok`.
+  uint32_t pend = 0;
+  bool pend_ok = false;
+  if (tid == 0 && p.sched) {
+    // static round robin: workgroup b takes tiles b, b + grid, ...  (all
+    // workgroups are co-resident, so the look-back still always progresses)
+    *s_ticket = blockIdx.x;
+    pend = blockIdx.x + gridDim.x;
+  } else if (tid == 0) {
+    const uint32_t t0 = atomicAdd(p.ticket, 1u);
+    if (t0 == p.nsuper + gridDim.x - 1)
+      __hip_atomic_store(p.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *s_ticket = t0;
+    if (t0 < p.nsuper) {
+      pend = atomicAdd(p.ticket, 1u);
+      pend_ok = true;
+    }
   }
   __syncthreads();
 
@@ -591,10 +756,10 @@ __global__ __launch_bounds__(TB) void gh_decode_kernel(const DecodeParams p) {
   uint32_t cur = *s_ticket;
   uint4 w[U];
   uint32_t w4[U];
+  uint32_t gw[U];
   int start[U];
   bool act[U];
-  if (cur < p.nsuper) load_tile<U>(p, cur, tid, w, w4, start, act);
-  bool seen_end = false;
+  load_tile<U>(p, cur, tid, w, w4, gw, act);
   uint32_t bad = 0;  // invalid bit pattern met (no-fallback build)
   bool have_prev = false;
   uint32_t prev = 0, prev_total = 0;
@@ -608,12 +773,11 @@ __global__ __launch_bounds__(TB) void gh_decode_kernel(const DecodeParams p) {
       if (tid == 0) atomicOr(p.status, (unsigned)GH_ST_TIMEOUT);
       break;
     }
-    if (!have_cur && !seen_end) {
-      seen_end = true;  // first out-of-range ticket: the last drawer resets the counter
-      if (tid == 0 && cur == p.nsuper + gridDim.x - 1)
-        __hip_atomic_store(p.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
     if (!have_cur && !have_prev) break;
+#ifdef GH_STAMPS
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): time spent waiting for tile loads/stores
+    STAMP(7);
+#endif
 
     // ---- decode / count tile k ----------------------------------------------------
     uint32_t cnt[U];
@@ -622,9 +786,21 @@ __global__ __launch_bounds__(TB) void gh_decode_kernel(const DecodeParams p) {
 #pragma unroll
     for (int u = 0; u < U; ++u) cnt[u] = 0;
     if (have_cur) {
+      tile_starts<U>(p, cur, tid, gw, start);
 #pragma unroll
       for (int u = 0; u < U; ++u) v[u] = make_win(w[u], w4[u], start[u]);
-      if constexpr (SINGLE) {
+      if (ABLATE(8)) {  // diagnostic: skip the decode, keep the output volume
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          cnt[u] = act[u] ? 16u : 0u;
+          if constexpr (SINGLE) {
+#pragma unroll
+            for (int k = 0; k < OW; ++k) ow[u][k] = k < 4 ? v[u].d0 : 0u;
+          }
+        }
+      } else if constexpr (G > 0) {
+        decode1g<U, G>(v, start, act, ow, cnt, smem, kshift - 3u);
+      } else if constexpr (SINGLE) {
         decode1_segments<FB, U>(v, start, act, ow, cnt, s_lut32, s_fb, kshift, p, bad);
       } else {
         count_segments<FB, U>(v, start, act, cnt, s_lut32, s_fb, kshift, p, bad);
@@ -652,9 +828,21 @@ __global__ __launch_bounds__(TB) void gh_decode_kernel(const DecodeParams p) {
       }
       bpos[u] += before + 16u;  // 16-byte zero pad in front of the staged tile
     }
-    if (tid == 0) {
+    if (tid == 0 && p.sched) {
       if (have_cur) publish_aggregate(p, cur, cur_total);
-      *s_ticket = have_cur ? atomicAdd(p.ticket, 1u) : 0xFFFFFFFFu;
+      *s_ticket = pend < p.nsuper ? pend : 0xFFFFFFFFu;
+      pend += gridDim.x;
+    } else if (tid == 0) {
+      if (have_cur) publish_aggregate(p, cur, cur_total);
+      // tickets are drawn one iteration ahead so the atomic's round trip is hidden;
+      // the drawer of the last out-of-range ticket resets the counter for the next
+      // launch (every workgroup draws exactly one out-of-range ticket)
+      const uint32_t t = pend_ok ? pend : 0xFFFFFFFFu;
+      if (t == p.nsuper + gridDim.x - 1)
+        __hip_atomic_store(p.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *s_ticket = t;
+      pend_ok = t < p.nsuper;
+      if (pend_ok) pend = atomicAdd(p.ticket, 1u);
     }
     // clear this iteration's staging buffer (it held tile k-2, copied out at k-1)
     {
@@ -666,28 +854,27 @@ __global__ __launch_bounds__(TB) void gh_decode_kernel(const DecodeParams p) {
     STAMP(2);
     const uint32_t next = *s_ticket;
     // the words of tile k are still needed by the emit pass (two-pass path)
+    // wave 0: issue the first look-back round of tile k-1 now; its fabric round
+    // trip overlaps the staging of tile k below
+    // look-back of tile k-1, first round issued by all four waves now: its fabric
+    // round trip overlaps the staging of tile k
+    const bool resolve = have_prev && !ABLATE(1);
+    unsigned long long lbg[4];
+    lookback_issue(p, prev, wid, lane, lbg);
+    // then the next tile's loads (after the look-back loads, so waiting for the
+    // look-back below does not wait for them)
     uint4 wn[U];
     uint32_t w4n[U];
-    int startn[U];
+    uint32_t gwn[U];
     bool actn[U];
-    if (next < p.nsuper) load_tile<U>(p, next, tid, wn, w4n, startn, actn);
-    if (have_prev && wid == 0) {
-      const unsigned long long ex = ABLATE(1) ? 0ull : resolve_prefix(p, prev, prev_total, lane);
-      if (lane == 0) {
-        *s_goff = ex;
-        if (prev == p.nsuper - 1) *p.total = ex + prev_total;
-      }
-    }
-    STAMP(3);
-    __syncthreads();  // B2: prefix of tile k-1
-    STAMP(4);
-    if (have_prev && !ABLATE(2))
-      copy_out_shifted(p, (const uint32_t*)(s_stage0 + (par ^ 1u) * p.stage_bytes), *s_goff,
-                       prev_total, tid);
-    STAMP(5);
+    load_tile<U>(p, next, tid, wn, w4n, gwn, actn);
+    __asm__ volatile("" ::: "memory");
     if (have_cur && !ABLATE(4)) {
       uint32_t* stg = (uint32_t*)(s_stage0 + par * p.stage_bytes);
-      if constexpr (SINGLE) {
+      if constexpr (G > 0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) stage_bytes_z(stg, ow[u], bpos[u]);
+      } else if constexpr (SINGLE) {
 #pragma unroll
         for (int u = 0; u < U; ++u)
           if (cnt[u]) stage_bytes(stg, ow[u], cnt[u], bpos[u]);
@@ -698,6 +885,43 @@ __global__ __launch_bounds__(TB) void gh_decode_kernel(const DecodeParams p) {
       }
     }
     STAMP(6);
+    if (resolve) lookback_summarise(p, prev, wid, lane, lbg, &s_lb[wid]);
+    STAMP(3);
+    __syncthreads();  // B2: tile k staged, look-back summaries of tile k-1
+    STAMP(4);
+    unsigned long long goff = 0;
+    if (resolve) {
+      // combine the four wave summaries (uniform across the workgroup)
+      bool good = true, done = false;
+#pragma unroll
+      for (int q = 0; q < NWAVE; ++q) {
+        const LbSummary sq = s_lb[q];
+        if (!done && good) {
+          good = sq.ok != 0;
+          goff += sq.sum;
+          done = good && sq.fp < 256;
+        }
+      }
+      if (!done) {  // rare: predecessors not published yet, or prefix farther back
+        if (wid == 0) {
+          const unsigned long long ex = resolve_slow(p, (long long)prev - 1, 0ull, lane);
+          if (lane == 0) *s_goff = ex;
+        }
+        __syncthreads();
+        goff = *s_goff;
+      }
+      if (tid == 0) {
+        __hip_atomic_store(&p.granules[prev], granule(p.epoch, 2, goff + prev_total),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == p.nsuper - 1) *p.total = goff + prev_total;
+      }
+    } else if (have_prev && tid == 0 && prev == p.nsuper - 1) {
+      *p.total = prev_total;  // ablation build only
+    }
+    if (have_prev && !ABLATE(2))
+      copy_out_shifted(p, (const uint32_t*)(s_stage0 + (par ^ 1u) * p.stage_bytes), goff,
+                       prev_total, tid);
+    STAMP(5);
     have_prev = have_cur;
     prev = cur;
     prev_total = cur_total;
@@ -708,7 +932,7 @@ __global__ __launch_bounds__(TB) void gh_decode_kernel(const DecodeParams p) {
     for (int u = 0; u < U; ++u) {
       w[u] = wn[u];
       w4[u] = w4n[u];
-      start[u] = startn[u];
+      gw[u] = gwn[u];
       act[u] = actn[u];
     }
   }
@@ -725,6 +949,8 @@ struct Tables {
   bool needs_fb = true;              // some codeword is longer than the LUT width K
   std::vector<uint2> lut;            // 2^K multi-symbol entries
   std::vector<uint32_t> lut1;        // 2^K single-symbol entries
+  std::vector<uint2> lut2;           // 2^K grouped-path entries {len, sym << 24}
+  int g = 0;                         // grouped single-symbol path: codewords per window shift
   uint32_t fb[FB_WORDS] = {};
   uint32_t fb_lo = 1, fb_hi = 1;
   uint32_t maxsyms_seg = 128;
@@ -797,7 +1023,8 @@ static int build_tables(const Canon& c, Tables& t, int force_k, int force_path) 
   if (c.nsyms == 0) return fail(GH_E_TABLE, "empty code");
   // Single-pass single-symbol path when every segment fits 32 symbols (minlen >= 4)
   // and 12-bit multi-symbol lookups would average < 1.5 symbols.
-  t.single = (force_path == 1) || (force_path != 2 && c.minlen >= 4 && multi_gain(c, 12) < 1.5);
+  t.single = (force_path == 1 || force_path == 3) ||
+             (force_path != 2 && c.minlen >= 4 && multi_gain(c, 12) < 1.5);
   if (c.minlen < 4) t.single = false;
   if (t.single) {
     t.K = force_k > 0 ? (uint32_t)std::clamp(force_k, 1, 12) : std::min<uint32_t>(c.maxlen, 12);
@@ -810,7 +1037,24 @@ static int build_tables(const Canon& c, Tables& t, int force_k, int force_path) 
     }
     t.lut.clear();
     if (t.lut1.size() < 4) t.lut1.resize(4, 0u);  // LDS copy moves 16-byte chunks
+    // grouped path: complete code (Kraft sum 1), all codewords within K bits
+    uint64_t kraft = 0;
+    for (uint32_t l = 1; l <= 16; ++l) kraft += (uint64_t)c.count[l] << (16 - l);
+    t.g = 0;
+    t.lut2.clear();
+    if (force_path != 3 && kraft == 65536 && c.maxlen <= t.K && c.maxlen <= 15) {
+      t.g = std::min<int>(4, 31 / (int)c.maxlen);
+      t.lut2.assign(1u << t.K, make_uint2(0, 0));
+      for (uint32_t i = 0; i < (1u << t.K); ++i) {
+        uint32_t fi = 0;
+        const uint32_t l = canon_decode16(c, (i << (32 - t.K)) >> 16, &fi);
+        t.lut2[i] = make_uint2(l, (uint32_t)c.sym[fi] << 24);
+      }
+      if (t.lut2.size() < 2) t.lut2.resize(2, make_uint2(0, 0));
+    }
   } else {
+    t.g = 0;
+    t.lut2.clear();
     t.K = force_k > 0 ? (uint32_t)std::clamp(force_k, 1, 12) : choose_k(c);
     t.lut.assign(1u << t.K, make_uint2(0, 0));
     for (uint32_t i = 0; i < (1u << t.K); ++i) {
@@ -859,20 +1103,29 @@ static void** args_of(DecodeParams& p) {
 template <bool SINGLE, bool FB>
 static const void* kernel_for_u(int uv) {
   switch (uv) {
-    case 4: return (const void*)gh_decode_kernel<SINGLE, FB, 4>;
-    case 2: return (const void*)gh_decode_kernel<SINGLE, FB, 2>;
-    default: return (const void*)gh_decode_kernel<SINGLE, FB, 1>;
+    case 4: return (const void*)gh_decode_kernel<SINGLE, FB, 4, 0>;
+    case 2: return (const void*)gh_decode_kernel<SINGLE, FB, 2, 0>;
+    default: return (const void*)gh_decode_kernel<SINGLE, FB, 1, 0>;
   }
 }
 
-// The no-fallback variants apply when every codeword fits the LUT width.
-static const void* kernel_for(bool single, bool fb, int uv) {
+template <int G>
+static const void* kernel_for_g(int uv) {
+  return uv >= 2 ? (const void*)gh_decode_kernel<true, false, 2, G>
+                 : (const void*)gh_decode_kernel<true, false, 1, G>;
+}
+
+// The no-fallback variants apply when every codeword fits the LUT width; the
+// grouped variants (g > 0) when the code is also complete.
+static const void* kernel_for(bool single, bool fb, int uv, int g = 0) {
+  if (g > 0) return g >= 4 ? kernel_for_g<4>(uv) : g == 3 ? kernel_for_g<3>(uv) : kernel_for_g<2>(uv);
   if (single) return fb ? kernel_for_u<true, true>(uv) : kernel_for_u<true, false>(uv);
   return fb ? kernel_for_u<false, true>(uv) : kernel_for_u<false, false>(uv);
 }
 
 struct gh_ctx {
   int device = 0;
+  size_t lut_bytes = 0;  // LDS bytes of the decode LUT of the loaded path
   hipStream_t stream = nullptr;
   int num_cu = 0;
   bool loaded = false;
@@ -948,6 +1201,10 @@ extern "C" int gh_ctx_create(int device, gh_ctx** out) {
       for (int sv : {1, 2, 4})
         (void)hipFuncSetAttribute(kernel_for(sg, fbv, sv),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  for (int gv : {2, 3, 4})
+    for (int sv : {1, 2})
+      (void)hipFuncSetAttribute(kernel_for(true, false, sv, gv),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   (void)hipGetLastError();
   *out = c;
   return GH_OK;
@@ -998,10 +1255,14 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
   c->ntiles = 0;
   c->grid = 0;
   if (c->nseg > 0) {
-    const size_t lut_bytes = c->tables.single ? c->tables.lut1.size() * sizeof(uint32_t)
-                                              : c->tables.lut.size() * sizeof(uint2);
-    const void* lut_src = c->tables.single ? (const void*)c->tables.lut1.data()
-                                           : (const void*)c->tables.lut.data();
+    const Tables& tb = c->tables;
+    const size_t lut_bytes = tb.g > 0    ? tb.lut2.size() * sizeof(uint2)
+                             : tb.single ? tb.lut1.size() * sizeof(uint32_t)
+                                         : tb.lut.size() * sizeof(uint2);
+    c->lut_bytes = lut_bytes;
+    const void* lut_src = tb.g > 0    ? (const void*)tb.lut2.data()
+                          : tb.single ? (const void*)tb.lut1.data()
+                                      : (const void*)tb.lut.data();
     GH_HIP(hipMalloc(&c->d_lut, std::max<size_t>(lut_bytes, 16)));
     GH_HIP(hipMemset(c->d_lut, 0, std::max<size_t>(lut_bytes, 16)));
     GH_HIP(hipMemcpy(c->d_lut, lut_src, lut_bytes, hipMemcpyHostToDevice));
@@ -1014,13 +1275,14 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
       const uint32_t per = TB * c->tables.maxsyms_seg;
       uv = c->tables.single ? 2 : (4 * per <= 16384) ? 4 : (2 * per <= 16384) ? 2 : 1;
     }
+    if (c->tables.g > 0 && uv > 2) uv = 2;
     for (;; uv >>= 1) {  // fall back to a narrower ILP width if the kernel does not fit
       c->super = (uint32_t)uv;
       c->stage_bytes = (uint32_t)(((uint64_t)uv * TB * c->tables.maxsyms_seg + 64 + 15) & ~15ull);
       c->lds = lut_bytes + FB_BYTES + 2 * c->stage_bytes + SCRATCH_BYTES;
       int per_cu = 0;
       GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-          &per_cu, kernel_for(c->tables.single, c->tables.needs_fb, uv), TB, c->lds));
+          &per_cu, kernel_for(c->tables.single, c->tables.needs_fb, uv, c->tables.g), TB, c->lds));
       if (per_cu >= 1) {
         const uint64_t grid = (uint64_t)per_cu * c->num_cu;
         c->ntiles = (uint32_t)ceil_div(c->nseg, (uint64_t)uv * TB);
@@ -1151,8 +1413,7 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
   p.nsuper = c->ntiles;
   p.kbits = c->tables.K;
   p.epoch = c->epoch;
-  p.lut_bytes = (uint32_t)(c->tables.single ? c->tables.lut1.size() * sizeof(uint32_t)
-                                            : c->tables.lut.size() * sizeof(uint2));
+  p.lut_bytes = (uint32_t)c->lut_bytes;
   p.stage_bytes = c->stage_bytes;
   p.fb_lo = c->tables.fb_lo;
   p.fb_hi = c->tables.fb_hi;
@@ -1160,6 +1421,8 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
   {
     const char* ab = getenv("GH_ABLATE");
     p.ablate = ab ? (unsigned)atoi(ab) : 0u;
+    const char* sc = getenv("GH_SCHED");
+    p.sched = (sc && !strcmp(sc, "dynamic")) ? 0u : 1u;
   }
   std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
   if (timed) {
@@ -1172,7 +1435,8 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     }
     GH_HIP(hipEventRecord(ev.first, st));
   }
-  GH_HIP(hipLaunchKernel(kernel_for(c->tables.single, c->tables.needs_fb, (int)c->super),
+  GH_HIP(hipLaunchKernel(kernel_for(c->tables.single, c->tables.needs_fb, (int)c->super,
+                                    c->tables.g),
                          dim3(c->grid), dim3(TB),
                          args_of(p), c->lds, st));
   GH_HIP(hipGetLastError());

@@ -5,7 +5,7 @@ os.environ.setdefault("GAPHUFF_LIB", os.path.join(here, "..", "cse375-finalproj-
 sys.path.insert(0, os.path.join(here, "..", "cse375-finalproj-huffman-decoding_amd"))
 import numpy as np, gaphuff as gh
 L = gh.lib(); L.gh_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]; L.gh_debug_stamps.restype = ctypes.c_int
-names = ["decode", "bar0", "clr+bar1", "resolve", "bar2", "copyout", "stage", "-", "-", "top"]
+names = ["decode", "bar0", "clr+bar1", "resolve", "bar2", "copyout", "stage", "memwait", "-", "top"]
 cfgs = [a.split(":") for a in sys.argv[1:]] or [["cfg4", "1000000000", "0.1"], ["cfg3", "1000000000", "0.9"]]
 for name, n, r in cfgs:
     n = int(n); r = float(r)

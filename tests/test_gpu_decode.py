@@ -153,11 +153,13 @@ def test_config_1GB_bitexact(gpu, cfg):
     assert np.array_equal(out, data)
 
 
-@pytest.mark.parametrize("path", ["1", "2"])
+@pytest.mark.parametrize("path", ["1", "2", "3"])
 @pytest.mark.parametrize("u", ["1", "2", "4"])
 def test_decode_paths_and_ilp(gpu, orc, path, u, monkeypatch):
-    """Both decode paths (1 = single-pass single-symbol, 2 = count + emit with
-    multi-symbol lookups) and every ILP width give identical bytes."""
+    """Every decode path (1 = single-pass single-symbol, grouped window shifts when
+    the code is complete and fits the LUT; 2 = count + emit with multi-symbol
+    lookups; 3 = single-pass single-symbol without grouping) and every ILP width
+    give identical bytes."""
     monkeypatch.setenv("GH_PATH", path)
     monkeypatch.setenv("GH_U", u)
     cases = [gpu.generate(21, 0.1, 300_001), gpu.generate(22, 0.0, 77_777)]
