@@ -18,9 +18,11 @@ with the generated input.
 
 ``value`` = decoded bytes of all ranks per step x K / max-over-ranks wall time of the
 K steps (inputs resident in HBM).  ``roofline.achieved`` = algorithmic bytes per
-launch (compressed payload + gap words + decoded output) / the
-kernel's average duration, measured with HIP events recorded by the library on the
-stream the kernel is launched on (torch's current stream).  ``cpu_baseline`` times
+decode (compressed payload + gap words + decoded output) / the
+decode's average duration, measured with HIP events recorded by the library on the
+stream the kernels are launched on (torch's current stream).  A decode is one
+kernel (fused mode) or a count kernel followed by a write kernel (split mode);
+``roofline.mode`` says which.  ``cpu_baseline`` times
 the reference's own sequential.cpp (compiled from its sources into oracle/_ref by
 oracle/Makefile) on a bounded sample, rank 0 at N=1 only.
 """
@@ -220,7 +222,11 @@ def main() -> int:
                        "lut_bits": int(rep.lut_bits), "grid": int(rep.grid)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                         "traffic": traffic, "kernel": "gh::gh_decode_kernel",
+                         "traffic": traffic,
+                         "kernel": ("gh::gh_count_kernel + gh::gh_write_kernel"
+                                    if rep.mode == 1 else "gh::gh_decode_kernel"),
+                         "mode": gh.MODE_NAMES.get(int(rep.mode)),
+                         "path": gh.PATH_NAMES.get(int(rep.path)),
                          "kernel_ms": round(kern_ms, 4), "max_kernel_ms_over_ranks": round(max_kern, 4),
                          "alg_bytes_per_launch": alg,
                          "traffic_source": tsrc},

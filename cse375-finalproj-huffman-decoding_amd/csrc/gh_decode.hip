@@ -40,12 +40,13 @@
 
 namespace gh {
 
-constexpr int TB = 256;                  // workgroup size = segments per sub-tile
-constexpr int NWAVE = TB / 64;
+constexpr int TB = 256;                  // workgroup size of the multi-symbol paths
+constexpr int TB_G = 512;                // workgroup size of the grouped single-symbol path
+constexpr int MAX_NWAVE = TB_G / 64;
 constexpr int FB_WORDS = 3 * 17 + 64;    // limit16/base16/first + 256 symbol bytes
 constexpr int FB_BYTES = ((4 * FB_WORDS) + 15) & ~15;
 constexpr int MAX_SUPER = 8;             // sub-tiles per super-tile (template values 1,2,4,8)
-constexpr int SCRATCH_BYTES = 4 * (MAX_SUPER * NWAVE + 8) + 16 * NWAVE + 16;
+constexpr int SCRATCH_BYTES = 4 * (MAX_SUPER * MAX_NWAVE + 8) + 16 * MAX_NWAVE + 16;
 constexpr uint32_t EPOCH_MAX = (1u << 24) - 1;
 constexpr uint32_t SPIN_LIMIT = 1u << 18;
 
@@ -72,6 +73,12 @@ struct DecodeParams {
   unsigned long long* stamps;    // diagnostic build only (GH_STAMPS): per-block phase cycles
   unsigned int ablate;           // diagnostic build only: 1 no resolve, 2 no copy-out, 4 no stage
   unsigned int sched;            // 0: tiles from the atomic ticket; 1: static round robin
+  // split mode (count kernel -> scan kernel -> write kernel)
+  uint8_t* seg_cnt;              // codewords kept per segment (<= 128)
+  unsigned int* tile_cnt;        // codewords per tile
+  unsigned long long* tile_off;  // (unused)
+  unsigned long long* wg_tot;    // codewords per workgroup range (count kernel)
+  unsigned int count_per;        // count workgroups per write workgroup
 };
 #ifdef GH_STAMPS
 #define ABLATE(bit) (p.ablate & (bit))
@@ -430,17 +437,17 @@ __device__ __forceinline__ void lookback_summarise(const DecodeParams& p, uint32
 // Load the U segments of a tile owned by this thread (16-byte loads, coalesced).
 // The gap word is kept raw: extracting the nibble here would make the compiler
 // wait for the loads right away; tile_starts() does it when the tile is decoded.
-template <int U>
+template <int U, int TBK>
 __device__ __forceinline__ void load_tile(const DecodeParams& p, uint32_t tile, int tid,
                                           uint4 (&w)[U], uint32_t (&w4)[U], uint32_t (&gw)[U],
                                           bool (&act)[U]) {
   // Loads are unconditional (clamped to the last tile / segment): a load skipped
   // by a branch would make the compiler's wait counting fall back to vmcnt(0).
   const uint32_t t = min(tile, p.nsuper - 1);
-  const unsigned long long seg0 = (unsigned long long)t * (U * TB) + tid;
+  const unsigned long long seg0 = (unsigned long long)t * (U * TBK) + tid;
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    const unsigned long long seg = seg0 + (unsigned long long)u * TB;
+    const unsigned long long seg = seg0 + (unsigned long long)u * TBK;
     act[u] = tile < p.nsuper && seg < p.nseg;
     const unsigned long long sc = min(seg, p.nseg - 1);
     w[u] = *(const uint4*)(p.payload + 4 * sc);
@@ -451,13 +458,13 @@ __device__ __forceinline__ void load_tile(const DecodeParams& p, uint32_t tile, 
 
 // Start bit of each segment of the tile (its gap nibble, or first_start for the
 // shard's first segment).
-template <int U>
+template <int U, int TBK>
 __device__ __forceinline__ void tile_starts(const DecodeParams& p, uint32_t tile, int tid,
                                             const uint32_t (&gw)[U], int (&start)[U]) {
-  const unsigned long long seg0 = (unsigned long long)tile * (U * TB) + tid;
+  const unsigned long long seg0 = (unsigned long long)tile * (U * TBK) + tid;
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    const unsigned long long seg = seg0 + (unsigned long long)u * TB;
+    const unsigned long long seg = seg0 + (unsigned long long)u * TBK;
     const uint32_t nib = (uint32_t)(p.gap_nib0 + seg - 1) & 7u;
     start[u] = seg == 0 ? (int)p.first_start : (int)((gw[u] >> (4 * nib)) & 15u);
   }
@@ -658,13 +665,14 @@ __device__ __forceinline__ void stage_bytes(uint32_t* stg, const uint32_t (&ow)[
 // v_alignbyte (the tile's global offset is only known after its look-back, so the
 // staging cannot be pre-aligned); whole chunks go out as 16-byte stores, the two
 // edge chunks byte by byte.
+template <int TBK>
 __device__ __forceinline__ void copy_out_shifted(const DecodeParams& p, const uint32_t* stg32,
                                                  unsigned long long goff, uint32_t n, int tid) {
   const uint32_t lb = (uint32_t)(goff & 15);
   const unsigned long long a0 = goff - lb;
   const unsigned long long end = min(goff + n, p.out_cap);
   const uint32_t nz = (lb + n + 15u) >> 4;
-  for (uint32_t c = tid; c < nz; c += TB) {
+  for (uint32_t c = tid; c < nz; c += TBK) {
     const uint32_t sb = 16u * c + 16u - lb;  // staging byte of the chunk's first byte
     const uint32_t wi = sb >> 2, sh = sb & 3u;
     const uint32_t d0 = stg32[wi], d1 = stg32[wi + 1], d2 = stg32[wi + 2], d3 = stg32[wi + 3],
@@ -703,8 +711,9 @@ __device__ __forceinline__ void copy_out_shifted(const DecodeParams& p, const ui
 // drained it.  Three workgroup barriers per tile.
 //   SINGLE = true : single-symbol LUT, one decode pass, bytes held in registers
 //   SINGLE = false: multi-symbol LUT, count pass then emit pass.
-template <bool SINGLE, bool FB, int U, int G>
-__global__ __launch_bounds__(TB) void gh_decode_kernel(const DecodeParams p) {
+template <bool SINGLE, bool FB, int U, int G, int TBK>
+__global__ __launch_bounds__(TBK) void gh_decode_kernel(const DecodeParams p) {
+  constexpr int NWAVE = TBK / 64;
   static_assert(G == 0 || (SINGLE && !FB), "grouped path: single-symbol, no fallback");
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint2* s_lut = (const uint2*)smem;
@@ -712,8 +721,8 @@ __global__ __launch_bounds__(TB) void gh_decode_kernel(const DecodeParams p) {
   uint32_t* s_fb = (uint32_t*)(smem + p.lut_bytes);
   uint8_t* s_stage0 = smem + p.lut_bytes + FB_BYTES;
   uint32_t* s_scr = (uint32_t*)(s_stage0 + 2 * p.stage_bytes);
-  uint32_t* s_ticket = s_scr + MAX_SUPER * NWAVE;
-  unsigned long long* s_goff = (unsigned long long*)(s_scr + MAX_SUPER * NWAVE + 2);
+  uint32_t* s_ticket = s_scr + MAX_SUPER * MAX_NWAVE;
+  unsigned long long* s_goff = (unsigned long long*)(s_scr + MAX_SUPER * MAX_NWAVE + 2);
   LbSummary* s_lb = (LbSummary*)(s_goff + 1);
 
   const int tid = threadIdx.x;
@@ -723,10 +732,10 @@ __global__ __launch_bounds__(TB) void gh_decode_kernel(const DecodeParams p) {
   {
     const uint4* g = p.lut;
     uint4* s = (uint4*)smem;
-    for (uint32_t i = tid; i < p.lut_bytes / 16; i += TB) s[i] = g[i];
-    for (uint32_t i = tid; i < (uint32_t)FB_WORDS; i += TB) s_fb[i] = p.fb[i];
+    for (uint32_t i = tid; i < p.lut_bytes / 16; i += TBK) s[i] = g[i];
+    for (uint32_t i = tid; i < (uint32_t)FB_WORDS; i += TBK) s_fb[i] = p.fb[i];
     uint4* st = (uint4*)s_stage0;
-    for (uint32_t i = tid; i < 2 * p.stage_bytes / 16; i += TB) st[i] = make_uint4(0, 0, 0, 0);
+    for (uint32_t i = tid; i < 2 * p.stage_bytes / 16; i += TBK) st[i] = make_uint4(0, 0, 0, 0);
   }
   // thread 0: ticket drawn for the iteration after next.  `pend` is only ever
   // written by the atomic (a plain write would have to wait for it); whether a
@@ -759,7 +768,7 @@ __global__ __launch_bounds__(TB) void gh_decode_kernel(const DecodeParams p) {
   uint32_t gw[U];
   int start[U];
   bool act[U];
-  load_tile<U>(p, cur, tid, w, w4, gw, act);
+  load_tile<U, TBK>(p, cur, tid, w, w4, gw, act);
   uint32_t bad = 0;  // invalid bit pattern met (no-fallback build)
   bool have_prev = false;
   uint32_t prev = 0, prev_total = 0;
@@ -786,7 +795,7 @@ __global__ __launch_bounds__(TB) void gh_decode_kernel(const DecodeParams p) {
 #pragma unroll
     for (int u = 0; u < U; ++u) cnt[u] = 0;
     if (have_cur) {
-      tile_starts<U>(p, cur, tid, gw, start);
+      tile_starts<U, TBK>(p, cur, tid, gw, start);
 #pragma unroll
       for (int u = 0; u < U; ++u) v[u] = make_win(w[u], w4[u], start[u]);
       if (ABLATE(8)) {  // diagnostic: skip the decode, keep the output volume
@@ -848,7 +857,7 @@ __global__ __launch_bounds__(TB) void gh_decode_kernel(const DecodeParams p) {
     {
       uint4* st = (uint4*)(s_stage0 + par * p.stage_bytes);
       const uint32_t nclr = ((par ? used1 : used0) + 16u + 15u) >> 4;
-      for (uint32_t i = tid; i < nclr; i += TB) st[i] = make_uint4(0, 0, 0, 0);
+      for (uint32_t i = tid; i < nclr; i += TBK) st[i] = make_uint4(0, 0, 0, 0);
     }
     __syncthreads();  // B1: ticket, cleared buffer
     STAMP(2);
@@ -867,7 +876,7 @@ __global__ __launch_bounds__(TB) void gh_decode_kernel(const DecodeParams p) {
     uint32_t w4n[U];
     uint32_t gwn[U];
     bool actn[U];
-    load_tile<U>(p, next, tid, wn, w4n, gwn, actn);
+    load_tile<U, TBK>(p, next, tid, wn, w4n, gwn, actn);
     __asm__ volatile("" ::: "memory");
     if (have_cur && !ABLATE(4)) {
       uint32_t* stg = (uint32_t*)(s_stage0 + par * p.stage_bytes);
@@ -919,7 +928,7 @@ __global__ __launch_bounds__(TB) void gh_decode_kernel(const DecodeParams p) {
       *p.total = prev_total;  // ablation build only
     }
     if (have_prev && !ABLATE(2))
-      copy_out_shifted(p, (const uint32_t*)(s_stage0 + (par ^ 1u) * p.stage_bytes), goff,
+      copy_out_shifted<TBK>(p, (const uint32_t*)(s_stage0 + (par ^ 1u) * p.stage_bytes), goff,
                        prev_total, tid);
     STAMP(5);
     have_prev = have_cur;
@@ -938,6 +947,248 @@ __global__ __launch_bounds__(TB) void gh_decode_kernel(const DecodeParams p) {
   }
   if (!FB && __any(bad != 0) && lane == 0) atomicOr(p.status, (unsigned)GH_ST_BADCODE);
   STAMP_FLUSH;
+}
+
+// ============================================================================
+// Split mode: three kernels, no inter-workgroup waiting.
+//   gh_count_kernel  decodes each tile's segments counting codewords (no output),
+//                    writes the per-segment counts (1 byte each) and tile totals;
+//   gh_scan_kernel   exclusive prefix of the tile totals (one workgroup);
+//   gh_write_kernel  decodes each tile again, stages its bytes in LDS already at
+//                    the output's 16-byte alignment (its offset is known), and
+//                    copies them out with aligned 16-byte stores.
+// The compressed tile is read twice (C extra bytes of traffic), in exchange the
+// write kernel needs no look-back, no persistent loop and no funnel-shifted
+// copy-out, and every workgroup is independent (occupancy hides latency).
+// Reference counterpart: the fused count / scan / decode of gpu_dec_l1_l2
+// (decoder.cu:529-728).
+// ============================================================================
+template <int TBK>
+__device__ __forceinline__ void copy_lut_to_lds(const DecodeParams& p, uint8_t* smem, int tid) {
+  const uint4* g = p.lut;
+  uint4* s4 = (uint4*)smem;
+  for (uint32_t i = tid; i < p.lut_bytes / 16; i += TBK) s4[i] = g[i];
+  uint32_t* s_fb = (uint32_t*)(smem + p.lut_bytes);
+  for (uint32_t i = tid; i < (uint32_t)FB_WORDS; i += TBK) s_fb[i] = p.fb[i];
+}
+
+template <bool SINGLE, bool FB, int U, int G, int TBK>
+__device__ __forceinline__ void tile_decode(const DecodeParams& p, uint8_t* smem, Win (&v)[U],
+                                            const int (&start)[U], const bool (&act)[U],
+                                            uint32_t (&ow)[SINGLE ? U : 1][SINGLE ? OW : 1],
+                                            uint32_t (&cnt)[U], uint32_t& bad) {
+  const uint32_t kshift = 32u - p.kbits;
+  const uint32_t* s_lut32 = (const uint32_t*)smem;
+  const uint32_t* s_fb = (const uint32_t*)(smem + p.lut_bytes);
+  if (ABLATE(8)) {  // diagnostic: no decode, plausible output volume
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      cnt[u] = act[u] ? 16u : 0u;
+      if constexpr (SINGLE) {
+#pragma unroll
+        for (int k = 0; k < OW; ++k) ow[u][k] = k < 4 ? v[u].d0 : 0u;
+      }
+    }
+    return;
+  }
+  if constexpr (G > 0) {
+    decode1g<U, G>(v, start, act, ow, cnt, smem, kshift - 3u);
+  } else if constexpr (SINGLE) {
+    decode1_segments<FB, U>(v, start, act, ow, cnt, s_lut32, s_fb, kshift, p, bad);
+  } else {
+    count_segments<FB, U>(v, start, act, cnt, s_lut32, s_fb, kshift, p, bad);
+  }
+}
+
+// Tiles [t0, t1) of workgroup b: contiguous ranges of (almost) equal length.
+__device__ __forceinline__ void wg_range(uint32_t ntiles, uint32_t& t0, uint32_t& t1) {
+  t0 = (uint32_t)(((unsigned long long)blockIdx.x * ntiles) / gridDim.x);
+  t1 = (uint32_t)(((unsigned long long)(blockIdx.x + 1) * ntiles) / gridDim.x);
+}
+
+template <bool SINGLE, bool FB, int U, int G, int TBK>
+__global__ __launch_bounds__(TBK) void gh_count_kernel(const DecodeParams p) {
+  constexpr int NWAVE = TBK / 64;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  __shared__ uint32_t s_wsum[2][NWAVE];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  uint32_t t0, t1;
+  wg_range(p.nsuper, t0, t1);
+  uint4 w[U];
+  uint32_t w4[U], gw[U];
+  bool act[U];
+  if (t0 < t1) load_tile<U, TBK>(p, t0, tid, w, w4, gw, act);
+  copy_lut_to_lds<TBK>(p, smem, tid);
+  __syncthreads();
+  uint32_t bad = 0;
+  unsigned long long wg_total = 0;
+  uint32_t par = 0;
+  for (uint32_t t = t0; t < t1; ++t, par ^= 1u) {
+    int start[U];
+    tile_starts<U, TBK>(p, t, tid, gw, start);
+    Win v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = make_win(w[u], w4[u], start[u]);
+    bool a[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) a[u] = act[u];
+    if (t + 1 < t1) load_tile<U, TBK>(p, t + 1, tid, w, w4, gw, act);  // prefetch
+    uint32_t cnt[U];
+    uint32_t ow[SINGLE ? U : 1][SINGLE ? OW : 1];
+    tile_decode<SINGLE, FB, U, G, TBK>(p, smem, v, start, a, ow, cnt, bad);
+    const unsigned long long seg0 = (unsigned long long)t * (U * TBK) + tid;
+    uint32_t sum = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (a[u]) p.seg_cnt[seg0 + (unsigned long long)u * TBK] = (uint8_t)cnt[u];
+      sum += a[u] ? cnt[u] : 0u;
+    }
+    sum = wave_incl_scan(sum, lane);
+    if (lane == 63) s_wsum[par][wid] = sum;
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t tt = 0;
+#pragma unroll
+      for (int q = 0; q < NWAVE; ++q) tt += s_wsum[par][q];
+      p.tile_cnt[t] = tt;
+      wg_total += tt;
+    }
+  }
+  if (tid == 0) p.wg_tot[blockIdx.x] = wg_total;
+  if (!FB && __any(bad != 0) && lane == 0) atomicOr(p.status, (unsigned)GH_ST_BADCODE);
+}
+
+template <bool SINGLE, bool FB, int U, int G, int TBK>
+__global__ __launch_bounds__(TBK) void gh_write_kernel(const DecodeParams p) {
+  constexpr int NWAVE = TBK / 64;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  __shared__ uint32_t s_wsum[2][U * NWAVE];
+  __shared__ unsigned long long s_base[NWAVE];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  uint8_t* s_stage = smem + p.lut_bytes + FB_BYTES;
+  uint32_t t0, t1;
+  wg_range(p.nsuper, t0, t1);
+  uint4 w[U];
+  uint32_t w4[U], gw[U], c8[U];
+  bool act[U];
+  auto load_counts = [&](uint32_t t) {
+    const unsigned long long seg0 = (unsigned long long)t * (U * TBK) + tid;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const unsigned long long seg = min(seg0 + (unsigned long long)u * TBK, p.nseg - 1);
+      c8[u] = p.seg_cnt[seg];
+    }
+  };
+  if (t0 < t1) {
+    load_tile<U, TBK>(p, t0, tid, w, w4, gw, act);
+    load_counts(t0);
+  }
+  // output offset of this workgroup's range: the totals of the ranges before it
+  {
+    unsigned long long b = 0;
+    const uint32_t nb = blockIdx.x * p.count_per;
+    for (uint32_t i = tid; i < nb; i += TBK) b += p.wg_tot[i];
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) b += __shfl_xor(b, d, 64);
+    if (lane == 0) s_base[wid] = b;
+  }
+  copy_lut_to_lds<TBK>(p, smem, tid);
+  {
+    uint4* st = (uint4*)s_stage;
+    for (uint32_t i = tid; i < p.stage_bytes / 16; i += TBK) st[i] = make_uint4(0, 0, 0, 0);
+  }
+  __syncthreads();
+  unsigned long long goff = 0;
+#pragma unroll
+  for (int q = 0; q < NWAVE; ++q) goff += s_base[q];
+  uint32_t par = 0;
+  uint32_t* stg = (uint32_t*)s_stage;
+  const uint4* st4 = (const uint4*)s_stage;
+  for (uint32_t t = t0; t < t1; ++t, par ^= 1u) {
+    int start[U];
+    tile_starts<U, TBK>(p, t, tid, gw, start);
+    Win v[U];
+    bool a[U];
+    uint32_t cc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      v[u] = make_win(w[u], w4[u], start[u]);
+      a[u] = act[u];
+      cc[u] = a[u] ? c8[u] : 0u;
+    }
+    const uint32_t ttot = p.tile_cnt[t];
+    if (t + 1 < t1) {  // prefetch the next tile
+      load_tile<U, TBK>(p, t + 1, tid, w, w4, gw, act);
+      load_counts(t + 1);
+    }
+    const uint32_t lb = (uint32_t)(goff & 15);
+    uint32_t bpos[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t incl = wave_incl_scan(cc[u], lane);
+      if (lane == 63) s_wsum[par][u * NWAVE + wid] = incl;
+      bpos[u] = incl - cc[u];
+    }
+    __syncthreads();  // wave sums; the previous tile's copy-out and clear are done
+    {
+      uint32_t before = 0;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        uint32_t add = before;
+#pragma unroll
+        for (int q = 0; q < NWAVE; ++q) {
+          const uint32_t x = s_wsum[par][u * NWAVE + q];
+          add += (q < wid) ? x : 0u;
+          before += x;
+        }
+        bpos[u] += add + 16u + lb;
+      }
+    }
+    uint32_t bad = 0;
+    if constexpr (SINGLE) {
+      uint32_t cnt[U];
+      uint32_t ow[U][OW];
+      tile_decode<SINGLE, FB, U, G, TBK>(p, smem, v, start, a, ow, cnt, bad);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if constexpr (G > 0) {
+          if (a[u]) stage_bytes_z(stg, ow[u], bpos[u]);
+        } else {
+          if (cnt[u]) stage_bytes(stg, ow[u], cnt[u], bpos[u]);
+        }
+      }
+    } else {
+      const uint2* s_lut = (const uint2*)smem;
+      const uint32_t* s_fb = (const uint32_t*)(smem + p.lut_bytes);
+      emit_segments<FB, U>(v, start, a, bpos, s_lut, s_fb, 32u - p.kbits, p, stg);
+    }
+    __syncthreads();  // tile staged
+    // staging byte x <-> output byte a0 - 16 + x, a0 = goff - lb (16-byte aligned);
+    // each thread clears the chunks it copied (the next tile stages after the
+    // next barrier)
+    const unsigned long long a0 = goff - lb;
+    const unsigned long long end = min(goff + ttot, p.out_cap);
+    const uint32_t nz = (16u + lb + ttot + 15u) >> 4;
+    uint4* stw = (uint4*)s_stage;
+    for (uint32_t c = tid; c < nz + 1; c += TBK) {
+      const uint4 d = st4[c];
+      stw[c] = make_uint4(0, 0, 0, 0);
+      if (c == 0 || c >= nz) continue;
+      const unsigned long long gs = a0 - 16 + 16ull * c;
+      if (gs >= goff && gs + 16 <= end) {
+        *(uint4*)(p.out + gs) = d;
+      } else {
+        const uint8_t* bb = (const uint8_t*)&d;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const unsigned long long ga = gs + k;
+          if (ga >= goff && ga < end) p.out[ga] = bb[k];
+        }
+      }
+    }
+    goff += ttot;
+  }
+  if (blockIdx.x == gridDim.x - 1 && tid == 0) *p.total = goff;
 }
 
 // ============================================================================
@@ -1103,16 +1354,16 @@ static void** args_of(DecodeParams& p) {
 template <bool SINGLE, bool FB>
 static const void* kernel_for_u(int uv) {
   switch (uv) {
-    case 4: return (const void*)gh_decode_kernel<SINGLE, FB, 4, 0>;
-    case 2: return (const void*)gh_decode_kernel<SINGLE, FB, 2, 0>;
-    default: return (const void*)gh_decode_kernel<SINGLE, FB, 1, 0>;
+    case 4: return (const void*)gh_decode_kernel<SINGLE, FB, 4, 0, TB>;
+    case 2: return (const void*)gh_decode_kernel<SINGLE, FB, 2, 0, TB>;
+    default: return (const void*)gh_decode_kernel<SINGLE, FB, 1, 0, TB>;
   }
 }
 
 template <int G>
 static const void* kernel_for_g(int uv) {
-  return uv >= 2 ? (const void*)gh_decode_kernel<true, false, 2, G>
-                 : (const void*)gh_decode_kernel<true, false, 1, G>;
+  return uv >= 2 ? (const void*)gh_decode_kernel<true, false, 2, G, TB_G>
+                 : (const void*)gh_decode_kernel<true, false, 1, G, TB_G>;
 }
 
 // The no-fallback variants apply when every codeword fits the LUT width; the
@@ -1123,8 +1374,36 @@ static const void* kernel_for(bool single, bool fb, int uv, int g = 0) {
   return fb ? kernel_for_u<false, true>(uv) : kernel_for_u<false, false>(uv);
 }
 
+// Split-mode kernels: {count, write} for a path.  Workgroups of 256 threads.
+constexpr int TB_S = 256;
+struct SplitKernels {
+  const void* count;
+  const void* write;
+};
+template <bool SINGLE, bool FB, int U, int G>
+static SplitKernels split_pair() {
+  return {(const void*)gh_count_kernel<SINGLE, FB, U, G, TB_S>,
+          (const void*)gh_write_kernel<SINGLE, FB, U, G, TB_S>};
+}
+static SplitKernels split_for(bool single, bool fb, int uv, int g) {
+  if (g > 0)
+    return g >= 4 ? split_pair<true, false, 2, 4>()
+           : g == 3 ? split_pair<true, false, 2, 3>() : split_pair<true, false, 2, 2>();
+  if (single) return fb ? split_pair<true, true, 2, 0>() : split_pair<true, false, 2, 0>();
+  if (uv >= 2) return fb ? split_pair<false, true, 2, 0>() : split_pair<false, false, 2, 0>();
+  return fb ? split_pair<false, true, 1, 0>() : split_pair<false, false, 1, 0>();
+}
+
 struct gh_ctx {
   int device = 0;
+  bool split = true;       // split mode (count / scan / write) vs the fused persistent kernel
+  uint32_t count_per = 1;  // split mode: count workgroups per write workgroup
+  size_t lds_count = 0;    // split mode: dynamic LDS of the count / write kernels
+  uint8_t* d_seg_cnt = nullptr;
+  uint32_t* d_tile_cnt = nullptr;
+  unsigned long long* d_tile_off = nullptr;
+  unsigned long long* d_wg_tot = nullptr;
+  int tb = TB;           // workgroup size of the loaded path
   size_t lut_bytes = 0;  // LDS bytes of the decode LUT of the loaded path
   hipStream_t stream = nullptr;
   int num_cu = 0;
@@ -1162,6 +1441,14 @@ static void free_shard(gh_ctx* c) {
   (void)hipFree(c->d_lut);
   (void)hipFree(c->d_fb);
   (void)hipFree(c->d_stamps);
+  (void)hipFree(c->d_seg_cnt);
+  (void)hipFree(c->d_tile_cnt);
+  (void)hipFree(c->d_tile_off);
+  (void)hipFree(c->d_wg_tot);
+  c->d_wg_tot = nullptr;
+  c->d_seg_cnt = nullptr;
+  c->d_tile_cnt = nullptr;
+  c->d_tile_off = nullptr;
   c->d_stamps = nullptr;
   c->d_payload = nullptr;
   c->d_gaps = nullptr;
@@ -1205,6 +1492,14 @@ extern "C" int gh_ctx_create(int device, gh_ctx** out) {
     for (int sv : {1, 2})
       (void)hipFuncSetAttribute(kernel_for(true, false, sv, gv),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  for (int gv : {0, 2, 3, 4})
+    for (bool sg : {false, true})
+      for (bool fbv : {false, true})
+        for (int sv : {1, 2}) {
+          const SplitKernels k = split_for(sg, fbv, sv, gv);
+          (void)hipFuncSetAttribute(k.count, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+          (void)hipFuncSetAttribute(k.write, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        }
   (void)hipGetLastError();
   *out = c;
   return GH_OK;
@@ -1272,20 +1567,55 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
     const char* envu = getenv("GH_U");
     int uv = envu ? atoi(envu) : 0;
     if (uv != 1 && uv != 2 && uv != 4) {
-      const uint32_t per = TB * c->tables.maxsyms_seg;
+      const uint32_t per = TB * c->tables.maxsyms_seg;  // (multi-symbol paths)
       uv = c->tables.single ? 2 : (4 * per <= 16384) ? 4 : (2 * per <= 16384) ? 2 : 1;
     }
     if (c->tables.g > 0 && uv > 2) uv = 2;
-    for (;; uv >>= 1) {  // fall back to a narrower ILP width if the kernel does not fit
+    // Mode: the fused persistent kernel for the grouped single-symbol path, split
+    // kernels (count / write) for the others (measured faster on MI355X for each);
+    // GH_MODE=fused|split overrides.
+    const char* envm = getenv("GH_MODE");
+    c->split = envm ? !strcmp(envm, "split") : c->tables.g == 0;
+    if (c->split) {
+      // split mode: tiles of U*256 segments, U = 2 (single-symbol) or 1/2 (multi)
+      if (c->tables.single || c->tables.g > 0) uv = 2;
+      else if (!(envu && atoi(envu) == 2)) uv = (2u * TB_S * c->tables.maxsyms_seg <= 16384) ? 2 : 1;
+      c->tb = TB_S;
       c->super = (uint32_t)uv;
-      c->stage_bytes = (uint32_t)(((uint64_t)uv * TB * c->tables.maxsyms_seg + 64 + 15) & ~15ull);
+      c->stage_bytes = (uint32_t)(((uint64_t)uv * TB_S * c->tables.maxsyms_seg + 112 + 15) & ~15ull);
+      c->lds_count = lut_bytes + FB_BYTES;
+      c->lds = lut_bytes + FB_BYTES + c->stage_bytes;
+      c->ntiles = (uint32_t)ceil_div(c->nseg, (uint64_t)uv * TB_S);
+      const SplitKernels k = split_for(c->tables.single, c->tables.needs_fb, uv, c->tables.g);
+      int pc_c = 0, pc_w = 0;
+      GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc_c, k.count, TB_S, c->lds_count));
+      GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc_w, k.write, TB_S, c->lds));
+      if (pc_c < 1 || pc_w < 1) return fail(GH_E_HIP, "split decode kernels do not fit on a CU");
+      // both kernels walk the same contiguous tile ranges, one per workgroup
+      // The count kernel may run more workgroups: its ranges nest k to a write range
+      // (range boundaries floor(b*n/grid) coincide for grid_c = k*grid_w).
+      const char* envg = getenv("GH_GRID_PER_CU");
+      const int per_cu = envg ? std::max(1, atoi(envg)) : pc_w;
+      c->grid = (uint32_t)std::min<uint64_t>(c->ntiles, (uint64_t)per_cu * c->num_cu);
+      const uint32_t kk = std::max(1, pc_c / std::max(1, per_cu));
+      c->count_per = 1;
+      for (uint32_t k2 = kk; k2 >= 1; --k2)
+        if ((uint64_t)k2 * c->grid <= c->ntiles) { c->count_per = k2; break; }
+      GH_HIP(hipMalloc(&c->d_seg_cnt, c->nseg + 16));
+      GH_HIP(hipMalloc(&c->d_tile_cnt, 4ull * c->ntiles + 16));
+      GH_HIP(hipMalloc(&c->d_wg_tot, 8ull * c->grid * c->count_per + 16));
+    }
+    c->tb = c->split ? TB_S : c->tables.g > 0 ? TB_G : TB;
+    for (; !c->split; uv >>= 1) {  // fall back to a narrower ILP width if the kernel does not fit
+      c->super = (uint32_t)uv;
+      c->stage_bytes = (uint32_t)(((uint64_t)uv * c->tb * c->tables.maxsyms_seg + 64 + 15) & ~15ull);
       c->lds = lut_bytes + FB_BYTES + 2 * c->stage_bytes + SCRATCH_BYTES;
       int per_cu = 0;
       GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-          &per_cu, kernel_for(c->tables.single, c->tables.needs_fb, uv, c->tables.g), TB, c->lds));
+          &per_cu, kernel_for(c->tables.single, c->tables.needs_fb, uv, c->tables.g), c->tb, c->lds));
       if (per_cu >= 1) {
         const uint64_t grid = (uint64_t)per_cu * c->num_cu;
-        c->ntiles = (uint32_t)ceil_div(c->nseg, (uint64_t)uv * TB);
+        c->ntiles = (uint32_t)ceil_div(c->nseg, (uint64_t)uv * c->tb);
         c->grid = (uint32_t)std::min<uint64_t>(c->ntiles, grid);
         break;
       }
@@ -1435,10 +1765,22 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     }
     GH_HIP(hipEventRecord(ev.first, st));
   }
-  GH_HIP(hipLaunchKernel(kernel_for(c->tables.single, c->tables.needs_fb, (int)c->super,
-                                    c->tables.g),
-                         dim3(c->grid), dim3(TB),
-                         args_of(p), c->lds, st));
+  p.seg_cnt = c->d_seg_cnt;
+  p.tile_cnt = c->d_tile_cnt;
+  p.tile_off = c->d_tile_off;
+  p.wg_tot = c->d_wg_tot;
+  if (c->split) {
+    const SplitKernels k = split_for(c->tables.single, c->tables.needs_fb, (int)c->super,
+                                     c->tables.g);
+    p.count_per = c->count_per;
+    GH_HIP(hipLaunchKernel(k.count, dim3(c->grid * c->count_per), dim3(TB_S), args_of(p),
+                           c->lds_count, st));
+    GH_HIP(hipLaunchKernel(k.write, dim3(c->grid), dim3(TB_S), args_of(p), c->lds, st));
+  } else {
+    GH_HIP(hipLaunchKernel(kernel_for(c->tables.single, c->tables.needs_fb, (int)c->super,
+                                      c->tables.g),
+                           dim3(c->grid), dim3(c->tb), args_of(p), c->lds, st));
+  }
   GH_HIP(hipGetLastError());
   if (timed) {
     GH_HIP(hipEventRecord(ev.second, st));
@@ -1472,6 +1814,8 @@ extern "C" int gh_ctx_report(gh_ctx* c, void* hip_stream, gh_report* rep) {
     rep->lut_bits = c->tables.K;
     rep->grid = c->grid;
     rep->tiles = c->ntiles;
+    rep->mode = c->split ? GH_MODE_SPLIT : GH_MODE_FUSED;
+    rep->path = c->tables.g > 0 ? GH_PATH_GROUPED : c->tables.single ? GH_PATH_SINGLE : GH_PATH_MULTI;
     rep->launches = c->nlaunch;
     rep->kernel_ms = c->nlaunch ? (float)(c->acc_ms / c->nlaunch) : 0.f;
   }

@@ -80,7 +80,12 @@ class gh_report(ctypes.Structure):
         ("symbols", ctypes.c_uint64), ("out_bytes", ctypes.c_uint64), ("status", ctypes.c_uint32),
         ("lut_bits", ctypes.c_uint32), ("grid", ctypes.c_uint32), ("tiles", ctypes.c_uint32),
         ("kernel_ms", ctypes.c_float), ("launches", ctypes.c_uint32),
+        ("mode", ctypes.c_uint32), ("path", ctypes.c_uint32),
     ]
+
+
+MODE_NAMES = {0: "fused", 1: "split"}
+PATH_NAMES = {0: "multi", 1: "single", 2: "grouped"}
 
 
 class gh_opts(ctypes.Structure):

@@ -125,11 +125,19 @@ typedef struct gh_report {
   uint64_t out_bytes;      /* bytes written to the shard's device output           */
   uint32_t status;         /* device status bits (GH_ST_*)                          */
   uint32_t lut_bits;       /* K of the multi-symbol lookup table                    */
-  uint32_t grid;           /* persistent workgroups launched                        */
+  uint32_t grid;           /* workgroups launched (write kernel in split mode)      */
   uint32_t tiles;          /* segment tiles in the shard                            */
-  float kernel_ms;         /* average decode-kernel time of the recorded launches  */
-  uint32_t launches;       /* launches averaged in kernel_ms                        */
+  float kernel_ms;         /* average time of one decode (all its kernels), events  */
+  uint32_t launches;       /* decodes averaged in kernel_ms                         */
+  uint32_t mode;           /* GH_MODE_FUSED or GH_MODE_SPLIT                        */
+  uint32_t path;           /* GH_PATH_*: table / decode-loop variant                */
 } gh_report;
+
+#define GH_MODE_FUSED 0u    /* one persistent kernel, decoupled look-back            */
+#define GH_MODE_SPLIT 1u    /* count kernel + write kernel                           */
+#define GH_PATH_MULTI 0u    /* multi-symbol LUT, count + emit passes                 */
+#define GH_PATH_SINGLE 1u   /* single-symbol LUT, one pass (fallback for long codes) */
+#define GH_PATH_GROUPED 2u  /* single-symbol LUT, grouped window shifts              */
 
 #define GH_ST_BADCODE 1u    /* a bit pattern outside the code space was met       */
 #define GH_ST_TIMEOUT 2u    /* look-back spin gave up (never expected)            */

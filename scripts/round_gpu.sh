@@ -27,6 +27,11 @@ done
 step rocprof-stats
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_cfg2 -o run \
   -- python3 bench.py --cpu-sample 0 > $O/prof_cfg2.log 2>&1 || { tail $O/prof_cfg2.log; exit 1; }
+for w in cfg3 cfg4; do
+  step rocprof-stats-$w
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$w -o run \
+    -- python3 bench.py --workload $w --cpu-sample 0 > $O/prof_$w.log 2>&1 || { tail $O/prof_$w.log; exit 1; }
+done
 for c in FETCH_SIZE WRITE_SIZE; do
   step pmc-$c
   timeout -k 10 600 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $O/pmc_$c -o run \

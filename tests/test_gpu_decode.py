@@ -153,13 +153,16 @@ def test_config_1GB_bitexact(gpu, cfg):
     assert np.array_equal(out, data)
 
 
+@pytest.mark.parametrize("mode", ["fused", "split"])
 @pytest.mark.parametrize("path", ["1", "2", "3"])
 @pytest.mark.parametrize("u", ["1", "2", "4"])
-def test_decode_paths_and_ilp(gpu, orc, path, u, monkeypatch):
+def test_decode_paths_and_ilp(gpu, orc, path, u, mode, monkeypatch):
     """Every decode path (1 = single-pass single-symbol, grouped window shifts when
     the code is complete and fits the LUT; 2 = count + emit with multi-symbol
     lookups; 3 = single-pass single-symbol without grouping) and every ILP width
-    give identical bytes."""
+    give identical bytes, in both the fused persistent kernel and the split
+    count / write kernels."""
+    monkeypatch.setenv("GH_MODE", mode)
     monkeypatch.setenv("GH_PATH", path)
     monkeypatch.setenv("GH_U", u)
     cases = [gpu.generate(21, 0.1, 300_001), gpu.generate(22, 0.0, 77_777)]
@@ -172,6 +175,24 @@ def test_decode_paths_and_ilp(gpu, orc, path, u, monkeypatch):
     cases.append(g)  # minlen >= 4 with long codes -> fallback inside path 1
     for d in cases:
         _roundtrip(gpu, orc, d)
+
+
+@pytest.mark.parametrize("mode", ["fused", "split"])
+def test_dynamic_ticket_schedule(gpu, orc, mode, monkeypatch):
+    """The fused kernel's atomic-ticket tile schedule (GH_SCHED=dynamic) decodes the
+    same bytes as the default static schedule; repeated launches reuse the ticket."""
+    monkeypatch.setenv("GH_SCHED", "dynamic")
+    monkeypatch.setenv("GH_MODE", mode)
+    for r in (0.1, 0.5, 0.9):
+        data = gpu.generate(77, r, 2_000_003)
+        img = gpu.encode(data)
+        s = gpu.parse(img)
+        with gpu.Decoder(0) as d:
+            d.load(s)
+            for _ in range(3):
+                d.decode()
+            assert d.report().status == 0
+            assert np.array_equal(d.download(s.n), data)
 
 
 @pytest.mark.gpu
