@@ -336,7 +336,8 @@ __device__ __forceinline__ void publish_aggregate(const DecodeParams& p, uint32_
 // Slow path of the look-back (one wave): rounds of 256 granules from `base` down,
 // adding aggregates until an inclusive prefix; re-fetches while a predecessor
 // has not published.  Returns the exclusive prefix of `tile` (does not publish).
-__device__ unsigned long long resolve_slow(const DecodeParams& p, long long base,
+template <class P>
+__device__ unsigned long long resolve_slow(const P& p, long long base,
                                            unsigned long long excl, int lane) {
   constexpr unsigned long long VMASK = (1ull << 38) - 1;
   uint32_t spins = 0;
@@ -1192,6 +1193,547 @@ __global__ __launch_bounds__(TBK) void gh_write_kernel(const DecodeParams p) {
 }
 
 // ============================================================================
+// Tile mode: ONE persistent kernel, 512-thread workgroups, one segment per lane,
+// ONE workgroup barrier per tile.  Workgroup b takes tiles b, b + grid, ...
+// (static round robin; grid <= 512 and every workgroup resident).  Iteration k:
+//
+//   issue: look-back loads for tile k-1 (512 granules, one per lane: tiles
+//          k-1-1 .. k-1-512), then the loads of tile k+1
+//   decode tile k (registers) -> wave scan -> summarise the look-back per wave
+//   BARRIER
+//   publish aggregate(k); combine the 8 look-back summaries -> prefix of tile k-1,
+//   publish inclusive(k-1); copy tile k-1 out of staging buffer (k-1)&1;
+//   stage tile k into buffer k&1 at tile-local offsets
+//
+// Why the look-back spans 512 tiles and is one tile late: a granule stored on one
+// XCD becomes visible to another XCD's loads only after a fabric round trip, so a
+// look-back issued right after the predecessor publishes nearly always misses
+// (measured: 97% slow path).  One iteration later every predecessor of the round
+// has published its aggregate, and tile k-1-512 is this workgroup's own tile of
+// the previous round, whose inclusive prefix it published itself: the look-back
+// completes in one round of loads whose latency hides under the decode.
+//
+// Staging needs no clearing: a segment's bytes go to LDS as byte/short writes for
+// the partial head/tail dwords and dword writes in between, so no two lanes write
+// the same byte.  Buffer k&1 is staged after barrier k and copied out after barrier
+// k+1; its next staging is after barrier k+2.
+//
+// LUT: R = 2^lgr copies interleaved at dword granularity (entry i, copy c at
+// dword i*R + c; lane l reads copy l mod R), so up to 32 lanes of a ds_read_b32
+// group hit distinct banks.  The segment window is pre-shifted by
+// S = 30 - K - lgr bits (the "e-window"): the lookup address of the codeword at
+// window bit p is alignbit(e0, e1, 32 - p) & (mask << (2 + lgr)) | lane_offset,
+// two VALU ops.  Reference counterpart: gpu_dec_l1_l2 (decoder.cu:454-730).
+// ============================================================================
+#ifndef GH_TILE_TB
+#define GH_TILE_TB 512
+#endif
+constexpr int TB_T = GH_TILE_TB;
+constexpr int NWAVE_T = TB_T / 64;
+#ifndef GH_TILE_WPE
+#define GH_TILE_WPE 4
+#endif
+constexpr int STAGE_PAD = 16;  // staging byte STAGE_PAD + i = tile byte i
+#ifndef TILE_U
+#define TILE_U 2               // segments per lane (independent decode chains)
+#endif
+#ifndef GH_LB_MIDG
+#define GH_LB_MIDG 2           // decode group after which wave 0 checks the look-back
+#endif
+
+struct TileParams {
+  const uint32_t* payload;       // local segment j owns words [4j, 4j+4); +1 look-ahead, zero padded
+  const uint32_t* gaps;          // gap words; nibble (gap_nib0 + j - 1) = start of local segment j>=1
+  const uint32_t* lut;           // compact 2^K u32 entries {len | sym << 24}
+  uint8_t* out;
+  unsigned long long* granules;  // one per tile: its symbol count (flag 1)
+  unsigned long long* plocal;    // one per tile: exclusive prefix within its round (flag 2)
+  unsigned long long* rprefix;   // one per round: its starting offset (flag 2); [0] unused
+  unsigned int* status;
+  unsigned long long* total;
+  unsigned long long* stats;     // [0] slow look-backs (diagnostic counter)
+  unsigned long long out_cap;
+  unsigned long long nseg;
+  unsigned int gap_nib0, first_start, ntiles, kbits, lgr, epoch;
+  unsigned int lut_bytes;        // replicated LUT bytes in LDS = 4 << (K + lgr)
+  unsigned int stage_bytes;      // one staging buffer
+  unsigned long long* stamps;    // diagnostic build only (GH_STAMPS)
+  unsigned int ablate;           // diagnostic build only: 1 no look-back, 2 no copy-out, 4 no staging, 8 no decode
+};
+
+// e-window of a segment starting at bit `start` (0..15): e-stream bit 0 is segment
+// bit start - S (bits before the segment read as 0); requires 16 <= S <= 31.
+__device__ __forceinline__ void make_ewin(uint4 w, uint32_t w4, int start, uint32_t S,
+                                          uint32_t (&e)[5]) {
+  const uint32_t r = S - (uint32_t)start;  // 1..31
+  e[0] = __builtin_amdgcn_alignbit(0u, w.x, r);
+  e[1] = __builtin_amdgcn_alignbit(w.x, w.y, r);
+  e[2] = __builtin_amdgcn_alignbit(w.y, w.z, r);
+  e[3] = __builtin_amdgcn_alignbit(w.z, w.w, r);
+  e[4] = __builtin_amdgcn_alignbit(w.w, w4, r);
+}
+
+// LDS u32 read at an absolute LDS byte address, waited for at once (the lookups of a
+// segment form one dependent chain).  Inline asm: the compiler would otherwise add
+// the dynamic-LDS base (0 here: the tile kernel declares no static LDS, checked at
+// kernel start) with one extra VALU op per lookup.
+__device__ __forceinline__ uint32_t lds_u32(uint32_t byte_addr) {
+  uint32_t v;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(byte_addr) : "memory");
+  return v;
+}
+
+// LDS u32 read without a wait, and a wait that ties the results (so the compiler
+// cannot use them before it).  Used for the U independent lookups of a step.
+__device__ __forceinline__ uint32_t lds_u32_nowait(uint32_t byte_addr) {
+  uint32_t v;
+  asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"(byte_addr) : "memory");
+  return v;
+}
+template <int U>
+__device__ __forceinline__ void lds_wait_all(uint32_t (&v)[U]) {
+  if constexpr (U == 1) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]) :: "memory");
+  } else if constexpr (U == 2) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]) :: "memory");
+  } else {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]) :: "memory");
+  }
+}
+
+// Grouped single-symbol decode of U segments per lane on e-windows, the U chains in
+// lock-step (their LDS reads are independent, so their latencies overlap).  Each
+// group decodes G codewords per chain from e0:e1 and then shifts the windows;
+// codeword j of a chain is kept iff it starts before the segment end (q > T, see
+// decode1g); dead codewords insert 0.  `mid()` is called once, after group MIDG
+// (or at the end if the loop stops earlier): the tile kernel issues its look-back
+// loads there, late enough for its predecessors to have published.
+template <int G, int U, int MIDG, class Mid>
+__device__ __forceinline__ void decode_tile_grouped(uint32_t (&e)[U][5], const int (&start)[U],
+                                                    const bool (&act)[U], uint32_t (&ow)[U][OW],
+                                                    uint32_t (&cnt)[U], uint32_t amask,
+                                                    uint32_t laneoff, Mid&& mid) {
+  constexpr int S = 4 * OW;
+  constexpr int NG = (S + G - 1) / G;
+  uint32_t q[U];
+  int T[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    q[u] = 32;
+    T[u] = act[u] ? start[u] - 96 : 0x3FFFFFFF;  // inactive: never live, no overflow
+    cnt[u] = 0;
+#pragma unroll
+    for (int k = 0; k < OW; ++k) ow[u][k] = 0;
+  }
+  bool mid_done = false;
+#pragma unroll
+  for (int gi = 0; gi < NG; ++gi) {
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      const int pos = gi * G + j;
+      if (pos < S) {
+        uint32_t ent[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint32_t x = j == 0 ? e[u][0] : __builtin_amdgcn_alignbit(e[u][0], e[u][1], q[u]);
+          ent[u] = lds_u32_nowait((x & amask) | laneoff);
+        }
+        lds_wait_all(ent);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const bool live = (int)q[u] > T[u];
+          cnt[u] = live ? (uint32_t)(pos + 1) : cnt[u];
+          const uint32_t sb = live ? ent[u] : 0u;
+          ow[u][pos >> 2] = __builtin_amdgcn_perm(sb, ow[u][pos >> 2], perm_sel(pos & 3));
+          q[u] -= ent[u] & 31u;
+        }
+      }
+    }
+    bool more = false;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      e[u][0] = __builtin_amdgcn_alignbit(e[u][0], e[u][1], q[u]);
+      e[u][1] = __builtin_amdgcn_alignbit(e[u][1], e[u][2], q[u]);
+      e[u][2] = __builtin_amdgcn_alignbit(e[u][2], e[u][3], q[u]);
+      e[u][3] = __builtin_amdgcn_alignbit(e[u][3], e[u][4], q[u]);
+      e[u][4] = __builtin_amdgcn_alignbit(e[u][4], 0u, q[u]);
+      T[u] += 32 - (int)q[u];
+      q[u] = 32;
+      more |= 32 > T[u];
+    }
+    if (gi == MIDG) {
+      mid();
+      mid_done = true;
+    }
+    if (gi + 1 < NG && !__any(more)) break;
+  }
+  if (!mid_done) mid();
+}
+
+// Stage a segment's n bytes (ow, byte 0 first, zero past n) at LDS byte `pos`.
+// No two lanes write the same byte and nothing is ORed, so the buffer needs no
+// clearing: dwords wholly inside the segment are written by it; a dword shared with
+// the next segment (its partial tail) is written by this lane, combined with the
+// next lane's head bytes (a lane shuffle); a lane whose first dword is partial leaves
+// it to the previous lane.  Across a wave boundary (lane 63 -> next wave's lane 0)
+// the partial dword is written byte by byte by both sides.  Valid streams have >= 7
+// codewords per segment except the shard's last, so a dword never spans 3 segments.
+__device__ __forceinline__ void stage_exact(uint8_t* stg, const uint32_t (&ow)[OW], uint32_t n,
+                                            uint32_t pos, int lane) {
+  const uint32_t ph = pos & 3u;
+  const uint32_t sh = (32u - 8u * ph) & 31u;
+  // stream realigned to the LDS dword grid: dword m holds stream bytes [4m - ph, 4m - ph + 4)
+  const uint32_t x0 = ph ? __builtin_amdgcn_alignbit(ow[0], 0u, sh) : ow[0];
+  const uint32_t nxt = __shfl_down(ph ? x0 : 0u, 1, 64);  // next lane's head bytes (0 if none)
+  const uint32_t mfirst = ph ? 1u : 0u;
+  const uint32_t mend = (ph + n) >> 2;  // dwords [mfirst, mend) are wholly this segment's
+  uint32_t* base = (uint32_t*)(stg + (pos & ~3u));
+  uint32_t prev = 0, tw = 0;
+#pragma unroll
+  for (int m = 0; m <= OW; ++m) {
+    const uint32_t cur = m < OW ? ow[m] : 0u;
+    const uint32_t x = ph ? __builtin_amdgcn_alignbit(cur, prev, sh) : cur;
+    if ((uint32_t)m >= mfirst && (uint32_t)m < mend) base[m] = x;
+    tw = ((uint32_t)m == mend) ? x : tw;
+    prev = cur;
+  }
+  const uint32_t tn = (ph + n) & 3u;  // bytes of this segment in the tail dword
+  if (n != 0 && tn != 0 && mend >= mfirst) {
+    if (lane != 63) {
+      base[mend] = tw | nxt;
+    } else {
+      uint8_t* tp = (uint8_t*)(base + mend);
+      tp[0] = (uint8_t)tw;
+      if (tn > 1) tp[1] = (uint8_t)(tw >> 8);
+      if (tn > 2) tp[2] = (uint8_t)(tw >> 16);
+    }
+  }
+  if (lane == 0 && ph != 0 && n != 0) {  // head bytes shared with the previous wave's lane 63
+    const uint32_t hn = min(4u - ph, n);
+    stg[pos] = (uint8_t)ow[0];
+    if (hn > 1) stg[pos + 1] = (uint8_t)(ow[0] >> 8);
+    if (hn > 2) stg[pos + 2] = (uint8_t)(ow[0] >> 16);
+  }
+}
+
+// Copy a tile staged at staging byte STAGE_PAD + i = tile byte i to out[goff, goff+n)
+// (n already clamped at out_cap).  Output chunk c (16 bytes, aligned to the global
+// address) is staging bytes [16c + s, 16c + s + 16), s = 16 - (goff & 15): two
+// conflict-free ds_read_b128 and a funnel by the wave-uniform s.  Interior chunks
+// are one 16-byte store; the (at most two) partial edge chunks are finished byte by
+// byte by the lanes that own them.
+template <int TBK>
+__device__ __forceinline__ void copy_out_tile(uint8_t* out, const uint8_t* stg,
+                                              unsigned long long goff, uint32_t n, int tid) {
+  if (n == 0) return;
+  const uint4* st4 = (const uint4*)stg;
+  const uint32_t lb = (uint32_t)(goff & 15);
+  const uint32_t s = 16u - lb;             // 1..16, uniform
+  const uint32_t s4 = s >> 2, s1 = s & 3u;
+  uint8_t* o = out + (goff - lb);          // 16-byte aligned
+  const uint32_t nz = (lb + n + 15u) >> 4;
+  for (uint32_t c = tid; c < nz; c += TBK) {
+    const uint4 A = st4[c], B = st4[c + 1];
+    const uint32_t W[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+    uint4 v;
+    switch (s4) {  // wave-uniform
+      case 0:
+        v = make_uint4(__builtin_amdgcn_alignbyte(W[1], W[0], s1), __builtin_amdgcn_alignbyte(W[2], W[1], s1),
+                       __builtin_amdgcn_alignbyte(W[3], W[2], s1), __builtin_amdgcn_alignbyte(W[4], W[3], s1));
+        break;
+      case 1:
+        v = make_uint4(__builtin_amdgcn_alignbyte(W[2], W[1], s1), __builtin_amdgcn_alignbyte(W[3], W[2], s1),
+                       __builtin_amdgcn_alignbyte(W[4], W[3], s1), __builtin_amdgcn_alignbyte(W[5], W[4], s1));
+        break;
+      case 2:
+        v = make_uint4(__builtin_amdgcn_alignbyte(W[3], W[2], s1), __builtin_amdgcn_alignbyte(W[4], W[3], s1),
+                       __builtin_amdgcn_alignbyte(W[5], W[4], s1), __builtin_amdgcn_alignbyte(W[6], W[5], s1));
+        break;
+      case 3:
+        v = make_uint4(__builtin_amdgcn_alignbyte(W[4], W[3], s1), __builtin_amdgcn_alignbyte(W[5], W[4], s1),
+                       __builtin_amdgcn_alignbyte(W[6], W[5], s1), __builtin_amdgcn_alignbyte(W[7], W[6], s1));
+        break;
+      default:  // s == 16
+        v = make_uint4(W[4], W[5], W[6], W[7]);
+        break;
+    }
+    // tile bytes covered by this chunk: [16c - lb, 16c - lb + 16)
+    const int r0 = (int)(16u * c) - (int)lb;
+    if (r0 >= 0 && r0 + 16 <= (int)n) {
+      *(uint4*)(o + 16ull * c) = v;
+    } else {  // edge chunk: bytes [k0, k1) of it belong to the tile
+      const int k0 = max(0, -r0), k1 = min(16, (int)n - r0);
+      const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+      uint8_t* oc = o + 16ull * c;
+      for (int k = k0; k < k1; ++k) oc[k] = (uint8_t)(vv[k >> 2] >> (8 * (k & 3)));
+    }
+  }
+}
+
+// ---- prefixes by round leaders ------------------------------------------------
+// Tiles are processed in rounds: workgroup b takes tile rG + b in iteration r
+// (static round robin over the G resident workgroups).  A tile publishes its
+// symbol count (aggregate granule) right after its barrier.  Round r gets a leader,
+// workgroup r mod G, which during iteration r+1 loads the round's G aggregates (one
+// per lane, issued mid-decode: they were published a whole iteration earlier),
+// scans them at its barrier and publishes each tile's within-round exclusive prefix
+// (plocal) and the next round's starting offset R[r+1] = R[r] + round total.  The
+// owner of a tile reads R[round] + plocal[tile] at the top of iteration r+2 and
+// copies the tile out after its decode.  Every hand-off has about an iteration of
+// slack, and the granule traffic is three 8-byte loads/stores per tile (decoupled
+// look-back with 512 tiles in flight needs a window of ~512 granules per tile to
+// keep up: measured as the slow path of most tiles at 64/256).
+//
+// Granules: {epoch:24, flag:2, value:38} in one 8-byte word (the data is the flag).
+// Reference counterpart: the decoupled look-back of gpu_dec_l1_l2 (decoder.cu:601-653).
+constexpr int LDR_NB = TB_T / 64;  // leader batches: one wave per 64 tiles of a round
+
+// LDS of the tile kernel: replicated LUT, two staging buffers, wave sums, leader
+// batch totals.
+inline size_t tile_lds_bytes(size_t lut_bytes, size_t stage_bytes) {
+  return lut_bytes + 2 * stage_bytes + 2 * NWAVE_T * 4 * TILE_U + 4 * LDR_NB + 16 + 16;
+}
+
+// Poll a granule until it carries this launch's epoch with the wanted flag (bounded).
+__device__ __forceinline__ unsigned long long poll_granule(const TileParams& p,
+                                                           unsigned long long* g, uint32_t flag) {
+  for (uint32_t spins = 0;; ++spins) {
+    const unsigned long long v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((uint32_t)(v >> 40) == p.epoch && (uint32_t)((v >> 38) & 3u) == flag) return v;
+    if (spins > SPIN_LIMIT) {
+      atomicOr(p.status, (unsigned)GH_ST_TIMEOUT);
+      return 0;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+__device__ __forceinline__ bool granule_ok(const TileParams& p, unsigned long long v, uint32_t flag) {
+  return (uint32_t)(v >> 40) == p.epoch && (uint32_t)((v >> 38) & 3u) == flag;
+}
+
+template <int GRP>
+__global__ __launch_bounds__(TB_T) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE, 8)))
+void gh_tile_kernel(const TileParams p) {
+  constexpr int U = TILE_U;
+  constexpr unsigned long long VMASK = (1ull << 38) - 1;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* s_stage = smem + p.lut_bytes;                                   // 2 buffers
+  uint32_t* s_wsum = (uint32_t*)(s_stage + 2 * p.stage_bytes);             // [2][U][NWAVE_T]
+  uint32_t* s_lead = s_wsum + 2 * U * NWAVE_T;                             // [LDR_NB]
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  {  // replicate the LUT: dword i of LDS = entry i >> lgr
+    const uint32_t nd = p.lut_bytes >> 2;
+    uint32_t* sl = (uint32_t*)smem;
+    for (uint32_t i = tid; i < nd; i += TB_T) sl[i] = p.lut[i >> p.lgr];
+  }
+  const uint32_t S = 30u - p.kbits - p.lgr;
+  const uint32_t amask = ((1u << p.kbits) - 1u) << (2u + p.lgr);
+  const uint32_t laneoff = ((uint32_t)lane & ((1u << p.lgr) - 1u)) << 2;
+  if (tid == 0 && (uint32_t)(size_t)(const __attribute__((address_space(3))) uint8_t*)smem != 0u)
+    atomicOr(p.status, (unsigned)GH_ST_LAYOUT);
+  __syncthreads();
+
+  const uint32_t G = gridDim.x, b = blockIdx.x;  // grid size, workgroup
+  const uint32_t nseg = (uint32_t)p.nseg;  // < 2^31 (checked by the host)
+  const uint32_t nrounds = (p.ntiles + G - 1) / G;
+  constexpr uint32_t NONE = 0xFFFFFFFFu;
+  // Static round robin: tile b + kG in iteration k.  (A dynamic ticket order can
+  // deadlock here: a workgroup waiting for its tile's prefix may hold an undecoded
+  // tile of the same round, whose leader then waits for it.)
+  // The round led by this workgroup in iteration k is r = k - 1 when
+  // r mod n_r == b (n_r = tiles in round r), so every round has a leader that
+  // decoded one of its tiles.
+  const uint32_t last_tile_k = b < p.ntiles ? (p.ntiles - 1 - b) / G : NONE;
+  uint32_t cur = b, nxt = b + G;
+  STAMP_DECL
+  uint4 w[U];
+  uint32_t w4[U], gw[U];
+  auto load = [&](uint32_t t) {
+    const uint32_t seg0 = min(t, p.ntiles - 1) * (uint32_t)(U * TB_T) + (uint32_t)tid;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t sc = min(seg0 + (uint32_t)(u * TB_T), nseg - 1);
+      w[u] = *(const uint4*)(p.payload + 4ull * sc);
+      w4[u] = p.payload[4ull * sc + 4];
+      gw[u] = p.gaps[(p.gap_nib0 + (sc ? sc - 1u : 0u)) >> 3];
+    }
+  };
+  load(cur);
+  if (cur >= p.ntiles) cur = NONE;
+  uint32_t t1 = NONE, t2 = NONE;  // tiles of iterations k-1 and k-2
+  uint32_t tot1 = 0, tot2 = 0;    // their totals
+  uint32_t buf = 0;               // staging buffer of iteration k's tile (and of k-2's)
+  for (uint32_t k = 0;; ++k) {
+    const bool have_cur = cur < p.ntiles;
+    const bool have2 = t2 < p.ntiles;
+    // the workgroup that decoded tile rG + (r mod n_r) leads round r (n_r tiles) one
+    // iteration later: every round, the last partial one included, has a leader
+    const uint32_t lr = t1 < p.ntiles ? t1 / G : NONE;
+    const bool lead = lr != NONE && t1 % G == lr % min(G, p.ntiles - lr * G);
+    if (!have_cur && t1 >= p.ntiles && !have2) break;
+    if (last_tile_k != NONE && k > last_tile_k + 3) {  // cannot happen; never hang the GPU
+      if (tid == 0) atomicOr(p.status, (unsigned)GH_ST_TIMEOUT);
+      break;
+    }
+    const uint32_t par = k & 1u;
+    STAMP(9);
+    // prefix of tile k-2: R[round] + plocal[tile], read by lane 0 of every wave
+    unsigned long long gr = 0, gp = 0;
+    if (have2 && lane == 0) {
+      const uint32_t r2 = t2 / G;
+      gp = __hip_atomic_load(&p.plocal[t2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      gr = r2 == 0 ? 0ull
+                   : __hip_atomic_load(&p.rprefix[r2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    unsigned long long rl = 0;  // leader: R[lr] (wave 0 lane 0)
+    if (lead && tid == 0 && lr > 0)
+      rl = __hip_atomic_load(&p.rprefix[lr], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // leader: the round's aggregates, one per lane (issued mid-decode)
+    const uint32_t lt = lr * G + 64u * (uint32_t)wid + (uint32_t)lane;  // tile of this lane
+    const bool lvalid = lead && lt < min(p.ntiles, (lr + 1) * G);
+    unsigned long long la = 0;
+    auto mid = [&]() {
+      if (lead) la = __hip_atomic_load(&p.granules[lvalid ? lt : 0], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+    };
+    // ---- decode this tile (its words were loaded during the previous iteration) --
+    const uint32_t seg0 = cur * (uint32_t)(U * TB_T) + (uint32_t)tid;
+    uint32_t ow[U][OW], cnt[U];
+    {
+      int start[U];
+      bool act[U];
+      uint32_t e[U][5];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t seg = seg0 + (uint32_t)(u * TB_T);
+        act[u] = have_cur && seg < nseg;
+        const uint32_t nib = (p.gap_nib0 + seg - 1u) & 7u;
+        start[u] = seg == 0 ? (int)p.first_start : (int)((gw[u] >> (4 * nib)) & 15u);
+        make_ewin(w[u], w4[u], start[u], S, e[u]);
+      }
+      load(nxt);  // prefetch the next iteration's tile
+      if (have_cur && ABLATE(8)) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          cnt[u] = act[u] ? 16u : 0u;
+#pragma unroll
+          for (int k2 = 0; k2 < OW; ++k2) ow[u][k2] = k2 < 4 ? e[u][k2] : 0u;
+        }
+        mid();
+      } else if (have_cur) {
+        decode_tile_grouped<GRP, U, GH_LB_MIDG>(e, start, act, ow, cnt, amask, laneoff, mid);
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          cnt[u] = 0;
+#pragma unroll
+          for (int k2 = 0; k2 < OW; ++k2) ow[u][k2] = 0;
+        }
+        mid();
+      }
+    }
+    STAMP(0);
+    // ---- copy tile k-2 out (its prefix was published about an iteration ago) -------
+    if (have2) {
+      unsigned long long goff = 0;
+      if (lane == 0) {
+        const uint32_t r2 = t2 / G;
+        if (!granule_ok(p, gp, 2)) {
+          if (p.stats && wid == 0) atomicAdd(p.stats, 1ull);
+          gp = poll_granule(p, &p.plocal[t2], 2);
+        }
+        if (r2 > 0 && !granule_ok(p, gr, 2)) {
+          if (p.stats && wid == 0) atomicAdd(p.stats + 1, 1ull);
+          gr = poll_granule(p, &p.rprefix[r2], 2);
+        }
+        goff = (gp & VMASK) + (r2 > 0 ? (gr & VMASK) : 0ull);
+        if (wid == 0 && t2 == p.ntiles - 1) *p.total = goff + tot2;
+      }
+      goff = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(goff >> 32)) << 32) |
+             __builtin_amdgcn_readfirstlane((uint32_t)goff);
+      const uint32_t n2 = goff >= p.out_cap ? 0u : (uint32_t)min<unsigned long long>(tot2, p.out_cap - goff);
+      if (!ABLATE(2)) copy_out_tile<TB_T>(p.out, s_stage + buf * p.stage_bytes, goff, n2, tid);
+    }
+    STAMP(1);
+    uint32_t bpos[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t incl = wave_incl_scan(cnt[u], lane);
+      if (lane == 63) s_wsum[(par * U + u) * NWAVE_T + wid] = incl;
+      bpos[u] = incl - cnt[u];
+    }
+    // leader: every aggregate of the round published?  (rarely not: poll)
+    uint32_t lval = 0, lincl = 0;
+    if (lead) {
+      if (!__all(!lvalid || granule_ok(p, la, 1) || granule_ok(p, la, 2))) {
+        if (lane == 0 && p.stats) atomicAdd(p.stats + 2, 1ull);
+        if (lvalid && !(granule_ok(p, la, 1) || granule_ok(p, la, 2))) la = poll_granule(p, &p.granules[lt], 1);
+      }
+      lval = lvalid ? (uint32_t)(la & VMASK) : 0u;  // a tile holds < 2^32 symbols
+      lincl = wave_incl_scan(lval, lane);
+      if (lane == 63) s_lead[wid] = lincl;
+    }
+    STAMP(2);
+    __syncthreads();  // the one barrier: tile sums, leader batch totals
+    STAMP(3);
+    uint32_t tile_total = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      uint32_t add = tile_total;
+#pragma unroll
+      for (int q = 0; q < NWAVE_T; ++q) {
+        const uint32_t x = s_wsum[(par * U + u) * NWAVE_T + q];
+        add += (q < wid) ? x : 0u;
+        tile_total += x;
+      }
+      bpos[u] += add;
+    }
+    tile_total = __builtin_amdgcn_readfirstlane(tile_total);
+    if (tid == 0 && have_cur)
+      __hip_atomic_store(&p.granules[cur], granule(p.epoch, 1, tile_total), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    if (lead) {  // publish the round's within-round prefixes and R[lr + 1]
+      unsigned long long before = 0, total = 0;
+#pragma unroll
+      for (int q = 0; q < LDR_NB; ++q) {
+        const uint32_t x = s_lead[q];
+        before += (q < wid) ? x : 0u;
+        total += x;
+      }
+      if (lvalid)
+        __hip_atomic_store(&p.plocal[lt], granule(p.epoch, 2, before + lincl - lval),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (tid == 0) {
+        if (lr > 0 && !granule_ok(p, rl, 2)) {
+          if (p.stats) atomicAdd(p.stats + 3, 1ull);
+          rl = poll_granule(p, &p.rprefix[lr], 2);
+        }
+        const unsigned long long r0 = lr > 0 ? (rl & VMASK) : 0ull;
+        __hip_atomic_store(&p.rprefix[lr + 1], granule(p.epoch, 2, r0 + total), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    STAMP(4);
+    if (have_cur && !ABLATE(4)) {
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        stage_exact(s_stage + buf * p.stage_bytes, ow[u], cnt[u], STAGE_PAD + bpos[u], lane);
+    }
+    STAMP(5);
+    t2 = t1;
+    tot2 = tot1;
+    t1 = have_cur ? cur : NONE;
+    tot1 = tile_total;
+    buf ^= 1u;
+    cur = nxt < p.ntiles ? nxt : NONE;
+    nxt += G;
+  }
+  STAMP_FLUSH;
+}
+
+// ============================================================================
 // Host side
 // ============================================================================
 struct Tables {
@@ -1394,8 +1936,17 @@ static SplitKernels split_for(bool single, bool fb, int uv, int g) {
   return fb ? split_pair<false, true, 1, 0>() : split_pair<false, false, 1, 0>();
 }
 
+static const void* tile_kernel_for(uint32_t g) {
+  return g >= 4 ? (const void*)gh_tile_kernel<4>
+       : g == 3 ? (const void*)gh_tile_kernel<3> : (const void*)gh_tile_kernel<2>;
+}
+
 struct gh_ctx {
   int device = 0;
+  bool tile = false;       // tile mode (gh_tile_kernel); else split or fused
+  uint32_t tile_g = 0;     // tile mode: codewords per window shift
+  uint32_t lgr = 0;        // tile mode: log2 of the LUT replication
+  uint32_t* d_lut_t = nullptr;  // tile mode: compact u32 LUT
   bool split = true;       // split mode (count / scan / write) vs the fused persistent kernel
   uint32_t count_per = 1;  // split mode: count workgroups per write workgroup
   size_t lds_count = 0;    // split mode: dynamic LDS of the count / write kernels
@@ -1421,6 +1972,7 @@ struct gh_ctx {
   uint32_t* d_fb = nullptr;
   unsigned long long* d_stamps = nullptr;  // GH_STAMPS builds only
   uint32_t epoch = 0;
+  uint64_t gran_words = 0;  // u64 granules allocated at d_gran
   uint32_t ntiles = 0;   // super-tiles
   uint32_t super = 1;    // sub-tiles per super-tile (kernel template S)
   uint32_t grid = 0;
@@ -1445,6 +1997,8 @@ static void free_shard(gh_ctx* c) {
   (void)hipFree(c->d_tile_cnt);
   (void)hipFree(c->d_tile_off);
   (void)hipFree(c->d_wg_tot);
+  (void)hipFree(c->d_lut_t);
+  c->d_lut_t = nullptr;
   c->d_wg_tot = nullptr;
   c->d_seg_cnt = nullptr;
   c->d_tile_cnt = nullptr;
@@ -1481,8 +2035,8 @@ extern "C" int gh_ctx_create(int device, gh_ctx** out) {
   c->num_cu = prop.multiProcessorCount;
   GH_HIP(hipSetDevice(device));
   GH_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-  GH_HIP(hipMalloc(&c->d_misc, 64));
-  GH_HIP(hipMemset(c->d_misc, 0, 64));
+  GH_HIP(hipMalloc(&c->d_misc, 128));
+  GH_HIP(hipMemset(c->d_misc, 0, 128));
   for (bool sg : {false, true})
     for (bool fbv : {false, true})
       for (int sv : {1, 2, 4})
@@ -1492,6 +2046,9 @@ extern "C" int gh_ctx_create(int device, gh_ctx** out) {
     for (int sv : {1, 2})
       (void)hipFuncSetAttribute(kernel_for(true, false, sv, gv),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  for (uint32_t gv : {2u, 3u, 4u})
+    (void)hipFuncSetAttribute(tile_kernel_for(gv), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
   for (int gv : {0, 2, 3, 4})
     for (bool sg : {false, true})
       for (bool fbv : {false, true})
@@ -1545,7 +2102,7 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
   c->out_cap = out_cap;
   GH_HIP(hipSetDevice(c->device));
   GH_HIP(hipMalloc(&c->d_out, std::max<uint64_t>(out_cap, 16) + 64));
-  GH_HIP(hipMemset(c->d_misc, 0, 64));
+  GH_HIP(hipMemset(c->d_misc, 0, 128));
   c->epoch = 0;
   c->ntiles = 0;
   c->grid = 0;
@@ -1575,7 +2132,40 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
     // kernels (count / write) for the others (measured faster on MI355X for each);
     // GH_MODE=fused|split overrides.
     const char* envm = getenv("GH_MODE");
-    c->split = envm ? !strcmp(envm, "split") : c->tables.g == 0;
+    c->tile = c->tables.g > 0 && c->nseg < (1ull << 31) && (!envm || !strcmp(envm, "tile"));
+    c->split = !c->tile && (envm ? !strcmp(envm, "split") : c->tables.g == 0);
+    if (c->tile) {
+      // tile mode: compact LUT {len | sym << 24}, replicated 2^lgr times in LDS
+      const uint32_t K = c->tables.K;
+      c->tile_g = std::min<uint32_t>(4, 32 / std::max<uint32_t>(c->canon.maxlen, 1));
+      std::vector<uint32_t> lt(1u << K);
+      for (uint32_t i = 0; i < (1u << K); ++i) lt[i] = c->tables.lut2[i].x | c->tables.lut2[i].y;
+      GH_HIP(hipMalloc(&c->d_lut_t, 4ull << K));
+      GH_HIP(hipMemcpy(c->d_lut_t, lt.data(), 4ull << K, hipMemcpyHostToDevice));
+      c->tb = TB_T;
+      c->ntiles = (uint32_t)ceil_div(c->nseg, (uint64_t)TILE_U * TB_T);
+      c->stage_bytes =
+          (uint32_t)((STAGE_PAD + (uint64_t)TILE_U * TB_T * c->tables.maxsyms_seg + 48 + 15) & ~15ull);
+      const char* envr = getenv("GH_LGR");
+      int lg = envr ? std::clamp(atoi(envr), 0, 14 - (int)K) : std::min(5, 14 - (int)K);
+      // the largest replication that keeps the best occupancy
+      int per_cu = 0, best = 0, best_lg = 0;
+      for (int l2 = lg; l2 >= 0; --l2) {
+        const size_t lds = tile_lds_bytes(4ull << (K + l2), c->stage_bytes);
+        int pc = 0;
+        GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, tile_kernel_for(c->tile_g), TB_T, lds));
+        if (pc > best) { best = pc; best_lg = l2; }
+        if (envr) break;
+      }
+      lg = best_lg;
+      per_cu = best;
+      c->lut_bytes = 4ull << (K + lg);
+      c->lds = tile_lds_bytes(c->lut_bytes, c->stage_bytes);
+      if (per_cu < 1) return fail(GH_E_HIP, "tile decode kernel does not fit on a CU");
+      c->lgr = (uint32_t)lg;
+      c->super = 1;
+      c->grid = (uint32_t)std::min<uint64_t>(c->ntiles, (uint64_t)per_cu * c->num_cu);
+    }
     if (c->split) {
       // split mode: tiles of U*256 segments, U = 2 (single-symbol) or 1/2 (multi)
       if (c->tables.single || c->tables.g > 0) uv = 2;
@@ -1605,8 +2195,8 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
       GH_HIP(hipMalloc(&c->d_tile_cnt, 4ull * c->ntiles + 16));
       GH_HIP(hipMalloc(&c->d_wg_tot, 8ull * c->grid * c->count_per + 16));
     }
-    c->tb = c->split ? TB_S : c->tables.g > 0 ? TB_G : TB;
-    for (; !c->split; uv >>= 1) {  // fall back to a narrower ILP width if the kernel does not fit
+    if (!c->tile) c->tb = c->split ? TB_S : c->tables.g > 0 ? TB_G : TB;
+    for (; !c->split && !c->tile; uv >>= 1) {  // fall back to a narrower ILP width if the kernel does not fit
       c->super = (uint32_t)uv;
       c->stage_bytes = (uint32_t)(((uint64_t)uv * c->tb * c->tables.maxsyms_seg + 64 + 15) & ~15ull);
       c->lds = lut_bytes + FB_BYTES + 2 * c->stage_bytes + SCRATCH_BYTES;
@@ -1627,8 +2217,11 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
     GH_HIP(hipMemset(c->d_stamps, 0, 16ull * 8 * c->grid));
 #endif
   }
-  GH_HIP(hipMalloc(&c->d_gran, 8ull * std::max<uint32_t>(c->ntiles, 1)));
-  GH_HIP(hipMemset(c->d_gran, 0, 8ull * std::max<uint32_t>(c->ntiles, 1)));
+  // look-back granules; tile mode adds the within-round prefixes and the round offsets
+  c->gran_words = std::max<uint64_t>(c->ntiles, 1);
+  if (c->tile) c->gran_words = 2ull * c->ntiles + ceil_div(c->ntiles, std::max<uint32_t>(c->grid, 1)) + 2;
+  GH_HIP(hipMalloc(&c->d_gran, 8ull * c->gran_words));
+  GH_HIP(hipMemset(c->d_gran, 0, 8ull * c->gran_words));
   // start bit of local segment 0, and the gap nibble base for the rest
   c->first_start = 0;
   if (b > 0) {
@@ -1723,7 +2316,7 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     return GH_OK;
   }
   if (++c->epoch >= EPOCH_MAX) {  // granule epochs wrap: start clean
-    GH_HIP(hipMemsetAsync(c->d_gran, 0, 8ull * c->ntiles, st));
+    GH_HIP(hipMemsetAsync(c->d_gran, 0, 8ull * c->gran_words, st));
     c->epoch = 1;
   }
   DecodeParams p{};
@@ -1769,7 +2362,36 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
   p.tile_cnt = c->d_tile_cnt;
   p.tile_off = c->d_tile_off;
   p.wg_tot = c->d_wg_tot;
-  if (c->split) {
+  if (c->tile) {
+    TileParams t{};
+    t.payload = c->d_payload;
+    t.gaps = c->d_gaps;
+    t.lut = c->d_lut_t;
+    t.out = c->d_out;
+    t.granules = c->d_gran;
+    t.plocal = c->d_gran + c->ntiles;
+    t.rprefix = c->d_gran + 2ull * c->ntiles;
+    t.status = c->d_misc + 1;
+    t.total = (unsigned long long*)(c->d_misc + 2);
+    t.stats = (unsigned long long*)(c->d_misc + 4);
+    t.out_cap = c->out_cap;
+    t.nseg = c->nseg;
+    t.gap_nib0 = c->gap_nib0;
+    t.first_start = c->first_start;
+    t.ntiles = c->ntiles;
+    t.kbits = c->tables.K;
+    t.lgr = c->lgr;
+    t.epoch = c->epoch;
+    t.lut_bytes = (uint32_t)c->lut_bytes;
+    t.stage_bytes = c->stage_bytes;
+    t.stamps = c->d_stamps;
+    t.ablate = p.ablate;
+    static thread_local void* ta[1];
+    static thread_local TileParams tp;
+    tp = t;
+    ta[0] = &tp;
+    GH_HIP(hipLaunchKernel(tile_kernel_for(c->tile_g), dim3(c->grid), dim3(TB_T), ta, c->lds, st));
+  } else if (c->split) {
     const SplitKernels k = split_for(c->tables.single, c->tables.needs_fb, (int)c->super,
                                      c->tables.g);
     p.count_per = c->count_per;
@@ -1802,7 +2424,7 @@ extern "C" int gh_ctx_report(gh_ctx* c, void* hip_stream, gh_report* rep) {
     c->pool.push_back(e);
   }
   c->pending.clear();
-  unsigned int misc[4] = {};
+  unsigned int misc[6] = {};
   GH_HIP(hipMemcpy(misc, c->d_misc, sizeof(misc), hipMemcpyDeviceToHost));
   if (rep) {
     std::memset(rep, 0, sizeof(*rep));
@@ -1814,7 +2436,8 @@ extern "C" int gh_ctx_report(gh_ctx* c, void* hip_stream, gh_report* rep) {
     rep->lut_bits = c->tables.K;
     rep->grid = c->grid;
     rep->tiles = c->ntiles;
-    rep->mode = c->split ? GH_MODE_SPLIT : GH_MODE_FUSED;
+    rep->mode = c->tile ? GH_MODE_TILE : c->split ? GH_MODE_SPLIT : GH_MODE_FUSED;
+    std::memcpy(&rep->slow_lookbacks, misc + 4, 8);
     rep->path = c->tables.g > 0 ? GH_PATH_GROUPED : c->tables.single ? GH_PATH_SINGLE : GH_PATH_MULTI;
     rep->launches = c->nlaunch;
     rep->kernel_ms = c->nlaunch ? (float)(c->acc_ms / c->nlaunch) : 0.f;
@@ -1923,6 +2546,14 @@ extern "C" int gh_decode(const gh_stream* s, uint8_t* out, uint64_t out_len, con
 }
 
 #ifdef GH_STAMPS
+// Diagnostic build only: the tile kernel's look-back counters (cumulative).
+extern "C" int gh_debug_stats(gh_ctx* c, unsigned long long* host) {
+  if (!c || !host) return fail(GH_E_ARG, "null argument");
+  GH_HIP(hipDeviceSynchronize());
+  GH_HIP(hipMemcpy(host, c->d_misc + 4, 32, hipMemcpyDeviceToHost));
+  return GH_OK;
+}
+
 // Diagnostic build only: per-block phase cycle totals of the last launch.
 extern "C" int gh_debug_stamps(gh_ctx* c, unsigned long long* host, uint32_t max_blocks) {
   if (!c || !host || !c->d_stamps) return fail(GH_E_ARG, "no stamps");

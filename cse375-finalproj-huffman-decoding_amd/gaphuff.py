@@ -81,10 +81,11 @@ class gh_report(ctypes.Structure):
         ("lut_bits", ctypes.c_uint32), ("grid", ctypes.c_uint32), ("tiles", ctypes.c_uint32),
         ("kernel_ms", ctypes.c_float), ("launches", ctypes.c_uint32),
         ("mode", ctypes.c_uint32), ("path", ctypes.c_uint32),
+        ("slow_lookbacks", ctypes.c_uint64),
     ]
 
 
-MODE_NAMES = {0: "fused", 1: "split"}
+MODE_NAMES = {0: "fused", 1: "split", 2: "tile"}
 PATH_NAMES = {0: "multi", 1: "single", 2: "grouped"}
 
 

@@ -129,18 +129,21 @@ typedef struct gh_report {
   uint32_t tiles;          /* segment tiles in the shard                            */
   float kernel_ms;         /* average time of one decode (all its kernels), events  */
   uint32_t launches;       /* decodes averaged in kernel_ms                         */
-  uint32_t mode;           /* GH_MODE_FUSED or GH_MODE_SPLIT                        */
+  uint32_t mode;           /* GH_MODE_FUSED, GH_MODE_SPLIT or GH_MODE_TILE          */
   uint32_t path;           /* GH_PATH_*: table / decode-loop variant                */
+  uint64_t slow_lookbacks; /* tile mode: look-backs that needed the slow path        */
 } gh_report;
 
 #define GH_MODE_FUSED 0u    /* one persistent kernel, decoupled look-back            */
 #define GH_MODE_SPLIT 1u    /* count kernel + write kernel                           */
+#define GH_MODE_TILE 2u     /* persistent tile kernel, look-back per tile            */
 #define GH_PATH_MULTI 0u    /* multi-symbol LUT, count + emit passes                 */
 #define GH_PATH_SINGLE 1u   /* single-symbol LUT, one pass (fallback for long codes) */
 #define GH_PATH_GROUPED 2u  /* single-symbol LUT, grouped window shifts              */
 
 #define GH_ST_BADCODE 1u    /* a bit pattern outside the code space was met       */
 #define GH_ST_TIMEOUT 2u    /* look-back spin gave up (never expected)            */
+#define GH_ST_LAYOUT 4u     /* kernel LDS layout assumption violated (never expected) */
 
 /* Create a context on HIP device `device` (ordinal among visible devices). */
 int gh_ctx_create(int device, gh_ctx** out);
