@@ -131,8 +131,9 @@ __device__ __noinline__ uint32_t fallback_decode(const uint32_t* fb, uint32_t w1
   return ((uint32_t)syms[0] << 8) | hi;
 }
 
-__device__ __forceinline__ uint32_t fallback_meta(const uint32_t* fb, uint32_t t,
-                                                  const DecodeParams& p, uint32_t* syms) {
+template <class PRM>
+__device__ __forceinline__ uint32_t fallback_meta(const uint32_t* fb, uint32_t t, const PRM& p,
+                                                  uint32_t* syms) {
   const uint32_t r = fallback_decode(fb, t >> 16, p.fb_lo, p.fb_hi, p.status);
   *syms = r >> 8;
   return make_meta(1, r & 31u, 15, 15, 15);
@@ -1225,40 +1226,35 @@ __global__ __launch_bounds__(TBK) void gh_write_kernel(const DecodeParams p) {
 // window bit p is alignbit(e0, e1, 32 - p) & (mask << (2 + lgr)) | lane_offset,
 // two VALU ops.  Reference counterpart: gpu_dec_l1_l2 (decoder.cu:454-730).
 // ============================================================================
-#ifndef GH_TILE_TB
-#define GH_TILE_TB 512
-#endif
-constexpr int TB_T = GH_TILE_TB;
-constexpr int NWAVE_T = TB_T / 64;
-#ifndef GH_TILE_WPE
-#define GH_TILE_WPE 4
-#endif
 constexpr int STAGE_PAD = 16;  // staging byte STAGE_PAD + i = tile byte i
-#ifndef TILE_U
-#define TILE_U 2               // segments per lane (independent decode chains)
-#endif
 #ifndef GH_LB_MIDG
-#define GH_LB_MIDG 2           // decode group after which wave 0 checks the look-back
+#define GH_LB_MIDG 2           // decode group after which the round leader loads aggregates
 #endif
+// tile kernel paths
+constexpr int TP_GROUPED = 0;  // single-symbol u32 LUT on e-windows, grouped window shifts
+constexpr int TP_MULTI = 1;    // multi-symbol u64 LUT, count pass + emit pass
+constexpr int TP_MULTI_FB = 2; // the same with the canonical fallback for codes longer than K
 
 struct TileParams {
   const uint32_t* payload;       // local segment j owns words [4j, 4j+4); +1 look-ahead, zero padded
   const uint32_t* gaps;          // gap words; nibble (gap_nib0 + j - 1) = start of local segment j>=1
-  const uint32_t* lut;           // compact 2^K u32 entries {len | sym << 24}
+  const uint32_t* lut;           // grouped: 2^K u32 {len | sym << 24}; multi: 2^K u64 {syms, meta}
+  const uint32_t* fb;            // multi FB: canonical fallback tables (FB_WORDS)
   uint8_t* out;
   unsigned long long* granules;  // one per tile: its symbol count (flag 1)
   unsigned long long* plocal;    // one per tile: exclusive prefix within its round (flag 2)
   unsigned long long* rprefix;   // one per round: its starting offset (flag 2); [0] unused
   unsigned int* status;
   unsigned long long* total;
-  unsigned long long* stats;     // [0] slow look-backs (diagnostic counter)
+  unsigned long long* stats;     // poll counters (diagnostics)
   unsigned long long out_cap;
   unsigned long long nseg;
   unsigned int gap_nib0, first_start, ntiles, kbits, lgr, epoch;
-  unsigned int lut_bytes;        // replicated LUT bytes in LDS = 4 << (K + lgr)
+  unsigned int fb_lo, fb_hi;     // multi FB: fallback length range
+  unsigned int lut_bytes;        // LUT bytes in LDS (grouped: replicated 4 << (K + lgr))
   unsigned int stage_bytes;      // one staging buffer
   unsigned long long* stamps;    // diagnostic build only (GH_STAMPS)
-  unsigned int ablate;           // diagnostic build only: 1 no look-back, 2 no copy-out, 4 no staging, 8 no decode
+  unsigned int ablate;           // diagnostic build only: 2 no copy-out, 4 no staging, 8 no decode
 };
 
 // e-window of a segment starting at bit `start` (0..15): e-stream bit 0 is segment
@@ -1370,49 +1366,115 @@ __device__ __forceinline__ void decode_tile_grouped(uint32_t (&e)[U][5], const i
   if (!mid_done) mid();
 }
 
-// Stage a segment's n bytes (ow, byte 0 first, zero past n) at LDS byte `pos`.
-// No two lanes write the same byte and nothing is ORed, so the buffer needs no
-// clearing: dwords wholly inside the segment are written by it; a dword shared with
-// the next segment (its partial tail) is written by this lane, combined with the
-// next lane's head bytes (a lane shuffle); a lane whose first dword is partial leaves
-// it to the previous lane.  Across a wave boundary (lane 63 -> next wave's lane 0)
-// the partial dword is written byte by byte by both sides.  Valid streams have >= 7
-// codewords per segment except the shard's last, so a dword never spans 3 segments.
-__device__ __forceinline__ void stage_exact(uint8_t* stg, const uint32_t (&ow)[OW], uint32_t n,
-                                            uint32_t pos, int lane) {
-  const uint32_t ph = pos & 3u;
-  const uint32_t sh = (32u - 8u * ph) & 31u;
-  // stream realigned to the LDS dword grid: dword m holds stream bytes [4m - ph, 4m - ph + 4)
-  const uint32_t x0 = ph ? __builtin_amdgcn_alignbit(ow[0], 0u, sh) : ow[0];
-  const uint32_t nxt = __shfl_down(ph ? x0 : 0u, 1, 64);  // next lane's head bytes (0 if none)
-  const uint32_t mfirst = ph ? 1u : 0u;
-  const uint32_t mend = (ph + n) >> 2;  // dwords [mfirst, mend) are wholly this segment's
-  uint32_t* base = (uint32_t*)(stg + (pos & ~3u));
-  uint32_t prev = 0, tw = 0;
+// LDS u64 read (multi-symbol LUT entry) at an absolute LDS byte address.
+__device__ __forceinline__ uint2 lds_u64(uint32_t byte_addr) {
+  uint2 v;
+  asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(byte_addr) : "memory");
+  return v;
+}
+// LDS stores at absolute byte addresses.  ds_write_b32 may be unaligned: gfx950
+// LDS runs in unaligned mode and an unaligned dword store costs the same as an
+// aligned one (scripts/ubench/lds_unaligned.hip).
+__device__ __forceinline__ void lds_st32(uint32_t byte_addr, uint32_t v) {
+  asm volatile("ds_write_b32 %0, %1" :: "v"(byte_addr), "v"(v) : "memory");
+}
+__device__ __forceinline__ void lds_st8(uint32_t byte_addr, uint32_t v) {
+  asm volatile("ds_write_b8 %0, %1" :: "v"(byte_addr), "v"(v) : "memory");
+}
+
+// Per-lane select by a lane mask (mask bit set: a), opaque to the optimiser.
+__device__ __forceinline__ uint32_t vsel(unsigned long long mask, uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(mask));
+  return r;
+}
+
+// Stage a segment's n bytes (ow, byte 0 first) at absolute LDS byte address `pos`:
+// the whole dwords as (mostly unaligned) dword stores, the last n & 3 bytes as byte
+// stores, so no byte outside [pos, pos + n) is touched and segments need no
+// coordination.
+__device__ __forceinline__ void stage_unaligned(const uint32_t (&ow)[OW], uint32_t n, uint32_t pos) {
+  const uint32_t nf = n >> 2;
 #pragma unroll
-  for (int m = 0; m <= OW; ++m) {
-    const uint32_t cur = m < OW ? ow[m] : 0u;
-    const uint32_t x = ph ? __builtin_amdgcn_alignbit(cur, prev, sh) : cur;
-    if ((uint32_t)m >= mfirst && (uint32_t)m < mend) base[m] = x;
-    tw = ((uint32_t)m == mend) ? x : tw;
-    prev = cur;
+  for (int m = 0; m < OW; ++m)
+    if ((uint32_t)m < nf) lds_st32(pos + 4u * m, ow[m]);
+  const uint32_t t = n & 3u;
+  if (t) {
+    // ow[nf], selected by a 3-level tree of opaque selects (a plain ?: tree is
+    // turned back into an indexed load, which puts ow[] in scratch memory)
+    const unsigned long long s1 = __ballot((nf & 1u) != 0), s2 = __ballot((nf & 2u) != 0),
+                             s4 = __ballot((nf & 4u) != 0);
+    const uint32_t a0 = vsel(s1, ow[1], ow[0]), a1 = vsel(s1, ow[3], ow[2]);
+    const uint32_t a2 = vsel(s1, ow[5], ow[4]), a3 = vsel(s1, ow[7], ow[6]);
+    const uint32_t b0 = vsel(s2, a1, a0), b1 = vsel(s2, a3, a2);
+    const uint32_t x = vsel(s4, b1, b0);
+    const uint32_t q = pos + 4u * nf;
+    lds_st8(q, x);
+    if (t > 1) lds_st8(q + 1, x >> 8);
+    if (t > 2) lds_st8(q + 2, x >> 16);
   }
-  const uint32_t tn = (ph + n) & 3u;  // bytes of this segment in the tail dword
-  if (n != 0 && tn != 0 && mend >= mfirst) {
-    if (lane != 63) {
-      base[mend] = tw | nxt;
-    } else {
-      uint8_t* tp = (uint8_t*)(base + mend);
-      tp[0] = (uint8_t)tw;
-      if (tn > 1) tp[1] = (uint8_t)(tw >> 8);
-      if (tn > 2) tp[2] = (uint8_t)(tw >> 16);
+}
+
+// ---- multi-symbol path ------------------------------------------------------------
+// Count pass: codewords of the segment (window v at bit `start`) that start before
+// bit 128, with the reference's segment rule (decoder.cu:529-569): the last lookup
+// may hold codewords past the segment end; kept_in_last() drops them.
+template <bool FB>
+__device__ __forceinline__ uint32_t count_chain(Win v, int start, bool act, uint32_t kshift,
+                                                const TileParams& p, const uint32_t* s_fb,
+                                                uint32_t& bad) {
+  int P = act ? start : 128, Plast = P;
+  uint32_t mlast = make_meta(1, 0, 15, 15, 15), cnt = 0;
+  do {
+    uint32_t meta = lds_u32(((v.d0 >> kshift) << 3) + 4u);
+    if constexpr (FB) {
+      if (meta_n(meta) == 0 && P < 128) {
+        uint32_t sy;
+        meta = fallback_meta(s_fb, v.d0, p, &sy);
+      }
     }
-  }
-  if (lane == 0 && ph != 0 && n != 0) {  // head bytes shared with the previous wave's lane 63
-    const uint32_t hn = min(4u - ph, n);
-    stg[pos] = (uint8_t)ow[0];
-    if (hn > 1) stg[pos + 1] = (uint8_t)(ow[0] >> 8);
-    if (hn > 2) stg[pos + 2] = (uint8_t)(ow[0] >> 16);
+    const bool live = P < 128;
+    if constexpr (!FB) bad |= (live && meta_n(meta) == 0) ? 1u : 0u;
+    cnt += live ? meta_n(meta) : 0u;
+    Plast = live ? P : Plast;
+    mlast = live ? meta : mlast;
+    P += FB ? (int)meta_b(meta) : max((int)meta_b(meta), 1);
+    consume(v, meta);
+  } while (__any(P < 128));
+  if (act) cnt -= meta_n(mlast) - kept_in_last(mlast, 128 - Plast);
+  return cnt;
+}
+
+// Emit pass: decode again and store the cnt bytes at absolute LDS byte address pos:
+// a lookup's (up to 4) symbols go out as one unaligned dword while they fit below
+// pos + cnt; the last < 4 bytes as byte stores.
+template <bool FB>
+__device__ __forceinline__ void emit_chain(Win v, int start, bool act, uint32_t cnt, uint32_t pos,
+                                           uint32_t kshift, const TileParams& p,
+                                           const uint32_t* s_fb) {
+  int P = act ? start : 128;
+  const uint32_t end = pos + cnt;
+  uint32_t cur = pos;
+  bool go = P < 128 && cur < end;
+  while (__any(go)) {
+    uint2 e = lds_u64((v.d0 >> kshift) << 3);
+    if constexpr (FB) {
+      if (meta_n(e.y) == 0 && go) e.y = fallback_meta(s_fb, v.d0, p, &e.x);
+    }
+    const uint32_t n = meta_n(e.y);
+    if (go && cur + 4u <= end) {
+      lds_st32(cur, e.x);
+    } else if (go) {  // the last bytes
+      const uint32_t t = min(end - cur, n);
+      lds_st8(cur, e.x);
+      if (t > 1) lds_st8(cur + 1, e.x >> 8);
+      if (t > 2) lds_st8(cur + 2, e.x >> 16);
+      if (t > 3) lds_st8(cur + 3, e.x >> 24);
+    }
+    cur += go ? n : 0u;
+    P += FB ? (int)meta_b(e.y) : max((int)meta_b(e.y), 1);
+    consume(v, e.y);
+    go = go && P < 128 && cur < end;
   }
 }
 
@@ -1463,9 +1525,12 @@ __device__ __forceinline__ void copy_out_tile(uint8_t* out, const uint8_t* stg,
       *(uint4*)(o + 16ull * c) = v;
     } else {  // edge chunk: bytes [k0, k1) of it belong to the tile
       const int k0 = max(0, -r0), k1 = min(16, (int)n - r0);
-      const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
       uint8_t* oc = o + 16ull * c;
-      for (int k = k0; k < k1; ++k) oc[k] = (uint8_t)(vv[k >> 2] >> (8 * (k & 3)));
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const uint32_t wv = k < 4 ? v.x : k < 8 ? v.y : k < 12 ? v.z : v.w;
+        if (k >= k0 && k < k1) oc[k] = (uint8_t)(wv >> (8 * (k & 3)));
+      }
     }
   }
 }
@@ -1486,12 +1551,10 @@ __device__ __forceinline__ void copy_out_tile(uint8_t* out, const uint8_t* stg,
 //
 // Granules: {epoch:24, flag:2, value:38} in one 8-byte word (the data is the flag).
 // Reference counterpart: the decoupled look-back of gpu_dec_l1_l2 (decoder.cu:601-653).
-constexpr int LDR_NB = TB_T / 64;  // leader batches: one wave per 64 tiles of a round
-
-// LDS of the tile kernel: replicated LUT, two staging buffers, wave sums, leader
-// batch totals.
+// LDS of the tile kernel: LUT, two staging buffers, wave sums, leader batch totals.
+template <int TB, int U>
 inline size_t tile_lds_bytes(size_t lut_bytes, size_t stage_bytes) {
-  return lut_bytes + 2 * stage_bytes + 2 * NWAVE_T * 4 * TILE_U + 4 * LDR_NB + 16 + 16;
+  return lut_bytes + 2 * stage_bytes + 2 * (TB / 64) * 4 * U + 4 * (TB / 64) + 32;
 }
 
 // Poll a granule until it carries this launch's epoch with the wanted flag (bounded).
@@ -1512,22 +1575,37 @@ __device__ __forceinline__ bool granule_ok(const TileParams& p, unsigned long lo
   return (uint32_t)(v >> 40) == p.epoch && (uint32_t)((v >> 38) & 3u) == flag;
 }
 
-template <int GRP>
-__global__ __launch_bounds__(TB_T) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE, 8)))
+// TB threads, U segments per lane, PATH (TP_*), GRP codewords per window shift
+// (grouped path).
+template <int TB, int U, int PATH, int GRP>
+__global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4)))
 void gh_tile_kernel(const TileParams p) {
-  constexpr int U = TILE_U;
+  constexpr int NWAVE_T = TB / 64;
+  constexpr int LDR_NB = TB / 64;  // leader batches: one wave per 64 tiles of a round
+  constexpr bool MULTI = PATH != TP_GROUPED;
+  constexpr bool FB = PATH == TP_MULTI_FB;
+  static_assert(!MULTI || U == 1, "multi-symbol path: one segment per lane");
   constexpr unsigned long long VMASK = (1ull << 38) - 1;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* s_stage = smem + p.lut_bytes;                                   // 2 buffers
   uint32_t* s_wsum = (uint32_t*)(s_stage + 2 * p.stage_bytes);             // [2][U][NWAVE_T]
   uint32_t* s_lead = s_wsum + 2 * U * NWAVE_T;                             // [LDR_NB]
+  uint32_t bad = 0;  // multi (no FB): an invalid bit pattern was met
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  {  // replicate the LUT: dword i of LDS = entry i >> lgr
+  uint32_t* s_fb = s_lead + LDR_NB;  // multi FB: fallback tables (FB_WORDS)
+  {  // LUT to LDS (grouped: replicated, dword i of LDS = entry i >> lgr)
     const uint32_t nd = p.lut_bytes >> 2;
     uint32_t* sl = (uint32_t*)smem;
-    for (uint32_t i = tid; i < nd; i += TB_T) sl[i] = p.lut[i >> p.lgr];
+    if constexpr (MULTI) {
+      for (uint32_t i = tid; i < nd; i += TB) sl[i] = p.lut[i];
+      if constexpr (FB)
+        for (uint32_t i = tid; i < (uint32_t)FB_WORDS; i += TB) s_fb[i] = p.fb[i];
+    } else {
+      for (uint32_t i = tid; i < nd; i += TB) sl[i] = p.lut[i >> p.lgr];
+    }
   }
+  const uint32_t kshift = 32u - p.kbits;
   const uint32_t S = 30u - p.kbits - p.lgr;
   const uint32_t amask = ((1u << p.kbits) - 1u) << (2u + p.lgr);
   const uint32_t laneoff = ((uint32_t)lane & ((1u << p.lgr) - 1u)) << 2;
@@ -1537,7 +1615,6 @@ void gh_tile_kernel(const TileParams p) {
 
   const uint32_t G = gridDim.x, b = blockIdx.x;  // grid size, workgroup
   const uint32_t nseg = (uint32_t)p.nseg;  // < 2^31 (checked by the host)
-  const uint32_t nrounds = (p.ntiles + G - 1) / G;
   constexpr uint32_t NONE = 0xFFFFFFFFu;
   // Static round robin: tile b + kG in iteration k.  (A dynamic ticket order can
   // deadlock here: a workgroup waiting for its tile's prefix may hold an undecoded
@@ -1551,10 +1628,10 @@ void gh_tile_kernel(const TileParams p) {
   uint4 w[U];
   uint32_t w4[U], gw[U];
   auto load = [&](uint32_t t) {
-    const uint32_t seg0 = min(t, p.ntiles - 1) * (uint32_t)(U * TB_T) + (uint32_t)tid;
+    const uint32_t seg0 = min(t, p.ntiles - 1) * (uint32_t)(U * TB) + (uint32_t)tid;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const uint32_t sc = min(seg0 + (uint32_t)(u * TB_T), nseg - 1);
+      const uint32_t sc = min(seg0 + (uint32_t)(u * TB), nseg - 1);
       w[u] = *(const uint4*)(p.payload + 4ull * sc);
       w4[u] = p.payload[4ull * sc + 4];
       gw[u] = p.gaps[(p.gap_nib0 + (sc ? sc - 1u : 0u)) >> 3];
@@ -1599,15 +1676,37 @@ void gh_tile_kernel(const TileParams p) {
                                        __HIP_MEMORY_SCOPE_AGENT);
     };
     // ---- decode this tile (its words were loaded during the previous iteration) --
-    const uint32_t seg0 = cur * (uint32_t)(U * TB_T) + (uint32_t)tid;
-    uint32_t ow[U][OW], cnt[U];
-    {
+    const uint32_t seg0 = cur * (uint32_t)(U * TB) + (uint32_t)tid;
+    uint32_t ow[MULTI ? 1 : U][MULTI ? 1 : OW], cnt[U];
+    // multi: the segment's words and start, kept for the emit pass after the barrier
+    uint4 mw[U];
+    uint32_t mw4[U];
+    int mstart[U];
+    bool mact[U];
+    if constexpr (MULTI) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t seg = seg0 + (uint32_t)(u * TB);
+        mact[u] = have_cur && seg < nseg;
+        const uint32_t nib = (p.gap_nib0 + seg - 1u) & 7u;
+        mstart[u] = seg == 0 ? (int)p.first_start : (int)((gw[u] >> (4 * nib)) & 15u);
+        mw[u] = w[u];
+        mw4[u] = w4[u];
+      }
+      load(nxt);  // prefetch the next iteration's tile
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        cnt[u] = (have_cur && !ABLATE(8))
+                     ? count_chain<FB>(make_win(mw[u], mw4[u], mstart[u]), mstart[u], mact[u], kshift, p, s_fb, bad)
+                     : (mact[u] ? 16u : 0u);
+      mid();
+    } else {
       int start[U];
       bool act[U];
       uint32_t e[U][5];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const uint32_t seg = seg0 + (uint32_t)(u * TB_T);
+        const uint32_t seg = seg0 + (uint32_t)(u * TB);
         act[u] = have_cur && seg < nseg;
         const uint32_t nib = (p.gap_nib0 + seg - 1u) & 7u;
         start[u] = seg == 0 ? (int)p.first_start : (int)((gw[u] >> (4 * nib)) & 15u);
@@ -1623,7 +1722,7 @@ void gh_tile_kernel(const TileParams p) {
         }
         mid();
       } else if (have_cur) {
-        decode_tile_grouped<GRP, U, GH_LB_MIDG>(e, start, act, ow, cnt, amask, laneoff, mid);
+        decode_tile_grouped<(GRP > 0 ? GRP : 2), U, GH_LB_MIDG>(e, start, act, ow, cnt, amask, laneoff, mid);
       } else {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -1654,7 +1753,7 @@ void gh_tile_kernel(const TileParams p) {
       goff = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(goff >> 32)) << 32) |
              __builtin_amdgcn_readfirstlane((uint32_t)goff);
       const uint32_t n2 = goff >= p.out_cap ? 0u : (uint32_t)min<unsigned long long>(tot2, p.out_cap - goff);
-      if (!ABLATE(2)) copy_out_tile<TB_T>(p.out, s_stage + buf * p.stage_bytes, goff, n2, tid);
+      if (!ABLATE(2)) copy_out_tile<TB>(p.out, s_stage + buf * p.stage_bytes, goff, n2, tid);
     }
     STAMP(1);
     uint32_t bpos[U];
@@ -1717,9 +1816,17 @@ void gh_tile_kernel(const TileParams p) {
     }
     STAMP(4);
     if (have_cur && !ABLATE(4)) {
+      // absolute LDS address of this tile's staging (the kernel's LDS starts at 0)
+      const uint32_t sbase = p.lut_bytes + buf * p.stage_bytes + STAGE_PAD;
 #pragma unroll
-      for (int u = 0; u < U; ++u)
-        stage_exact(s_stage + buf * p.stage_bytes, ow[u], cnt[u], STAGE_PAD + bpos[u], lane);
+      for (int u = 0; u < U; ++u) {
+        if constexpr (MULTI) {
+          emit_chain<FB>(make_win(mw[u], mw4[u], mstart[u]), mstart[u], mact[u], cnt[u], sbase + bpos[u],
+                         kshift, p, s_fb);
+        } else {
+          stage_unaligned(ow[MULTI ? 0 : u], cnt[u], sbase + bpos[u]);
+        }
+      }
     }
     STAMP(5);
     t2 = t1;
@@ -1730,6 +1837,7 @@ void gh_tile_kernel(const TileParams p) {
     cur = nxt < p.ntiles ? nxt : NONE;
     nxt += G;
   }
+  if (!FB && MULTI && __any(bad != 0) && lane == 0) atomicOr(p.status, (unsigned)GH_ST_BADCODE);
   STAMP_FLUSH;
 }
 
@@ -1936,15 +2044,23 @@ static SplitKernels split_for(bool single, bool fb, int uv, int g) {
   return fb ? split_pair<false, true, 1, 0>() : split_pair<false, false, 1, 0>();
 }
 
-static const void* tile_kernel_for(uint32_t g) {
-  return g >= 4 ? (const void*)gh_tile_kernel<4>
-       : g == 3 ? (const void*)gh_tile_kernel<3> : (const void*)gh_tile_kernel<2>;
+// Tile-mode kernel geometry: the grouped path runs 512-thread workgroups with two
+// segments per lane; the multi-symbol paths 1024-thread workgroups with one (their
+// staging is up to 64 bytes per segment).
+constexpr int TB_GRP = 512, U_GRP = 2, TB_MUL = 1024, U_MUL = 1;
+static const void* tile_kernel_for(int path, uint32_t g) {
+  if (path == TP_MULTI) return (const void*)gh_tile_kernel<TB_MUL, U_MUL, TP_MULTI, 0>;
+  if (path == TP_MULTI_FB) return (const void*)gh_tile_kernel<TB_MUL, U_MUL, TP_MULTI_FB, 0>;
+  return g >= 4 ? (const void*)gh_tile_kernel<TB_GRP, U_GRP, TP_GROUPED, 4>
+       : g == 3 ? (const void*)gh_tile_kernel<TB_GRP, U_GRP, TP_GROUPED, 3>
+                : (const void*)gh_tile_kernel<TB_GRP, U_GRP, TP_GROUPED, 2>;
 }
 
 struct gh_ctx {
   int device = 0;
   bool tile = false;       // tile mode (gh_tile_kernel); else split or fused
-  uint32_t tile_g = 0;     // tile mode: codewords per window shift
+  int tile_path = 0;       // tile mode: TP_*
+  uint32_t tile_g = 0;     // tile mode: codewords per window shift (grouped path)
   uint32_t lgr = 0;        // tile mode: log2 of the LUT replication
   uint32_t* d_lut_t = nullptr;  // tile mode: compact u32 LUT
   bool split = true;       // split mode (count / scan / write) vs the fused persistent kernel
@@ -2046,9 +2162,10 @@ extern "C" int gh_ctx_create(int device, gh_ctx** out) {
     for (int sv : {1, 2})
       (void)hipFuncSetAttribute(kernel_for(true, false, sv, gv),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  for (uint32_t gv : {2u, 3u, 4u})
-    (void)hipFuncSetAttribute(tile_kernel_for(gv), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
+  for (int tp : {TP_GROUPED, TP_MULTI, TP_MULTI_FB})
+    for (uint32_t gv : {2u, 3u, 4u})
+      (void)hipFuncSetAttribute(tile_kernel_for(tp, gv), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024);
   for (int gv : {0, 2, 3, 4})
     for (bool sg : {false, true})
       for (bool fbv : {false, true})
@@ -2096,6 +2213,13 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
     const char* envp = getenv("GH_PATH");
     rc = build_tables(c->canon, c->tables, envk ? atoi(envk) : 0, envp ? atoi(envp) : 0);
     if (rc) return rc;
+    // tile mode runs the grouped single-symbol path or the multi-symbol paths
+    const char* envm0 = getenv("GH_MODE");
+    if (c->nseg < (1ull << 31) && envm0 && !strcmp(envm0, "tile") && c->tables.g == 0 &&
+        c->tables.single) {
+      rc = build_tables(c->canon, c->tables, envk ? atoi(envk) : 0, 2);
+      if (rc) return rc;
+    }
   }
   const uint64_t bound = c->nseg * (uint64_t)std::max<uint32_t>(c->tables.maxsyms_seg, 1);
   if (out_cap == 0) out_cap = std::min<uint64_t>(s->n, bound);
@@ -2132,39 +2256,79 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
     // kernels (count / write) for the others (measured faster on MI355X for each);
     // GH_MODE=fused|split overrides.
     const char* envm = getenv("GH_MODE");
-    c->tile = c->tables.g > 0 && c->nseg < (1ull << 31) && (!envm || !strcmp(envm, "tile"));
+    // Mode: the tile kernel for the grouped single-symbol path (and for any path with
+    // GH_MODE=tile); split kernels otherwise (measured faster for the multi-symbol
+    // paths, whose tile staging allows one workgroup per CU).  GH_MODE=fused|split
+    // override.
+    c->tile = c->nseg < (1ull << 31) && (envm ? !strcmp(envm, "tile") : c->tables.g > 0);
     c->split = !c->tile && (envm ? !strcmp(envm, "split") : c->tables.g == 0);
     if (c->tile) {
-      // tile mode: compact LUT {len | sym << 24}, replicated 2^lgr times in LDS
-      const uint32_t K = c->tables.K;
-      c->tile_g = std::min<uint32_t>(4, 32 / std::max<uint32_t>(c->canon.maxlen, 1));
-      std::vector<uint32_t> lt(1u << K);
-      for (uint32_t i = 0; i < (1u << K); ++i) lt[i] = c->tables.lut2[i].x | c->tables.lut2[i].y;
-      GH_HIP(hipMalloc(&c->d_lut_t, 4ull << K));
-      GH_HIP(hipMemcpy(c->d_lut_t, lt.data(), 4ull << K, hipMemcpyHostToDevice));
-      c->tb = TB_T;
-      c->ntiles = (uint32_t)ceil_div(c->nseg, (uint64_t)TILE_U * TB_T);
+      const bool grouped = c->tables.g > 0;
+      c->tile_path = grouped ? TP_GROUPED : c->tables.needs_fb ? TP_MULTI_FB : TP_MULTI;
+      const int TB = grouped ? TB_GRP : TB_MUL, U = grouped ? U_GRP : U_MUL;
+      c->tb = TB;
+      c->super = (uint32_t)U;
+      c->ntiles = (uint32_t)ceil_div(c->nseg, (uint64_t)U * TB);
       c->stage_bytes =
-          (uint32_t)((STAGE_PAD + (uint64_t)TILE_U * TB_T * c->tables.maxsyms_seg + 48 + 15) & ~15ull);
-      const char* envr = getenv("GH_LGR");
-      int lg = envr ? std::clamp(atoi(envr), 0, 14 - (int)K) : std::min(5, 14 - (int)K);
-      // the largest replication that keeps the best occupancy
-      int per_cu = 0, best = 0, best_lg = 0;
-      for (int l2 = lg; l2 >= 0; --l2) {
-        const size_t lds = tile_lds_bytes(4ull << (K + l2), c->stage_bytes);
-        int pc = 0;
-        GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, tile_kernel_for(c->tile_g), TB_T, lds));
-        if (pc > best) { best = pc; best_lg = l2; }
-        if (envr) break;
+          (uint32_t)((STAGE_PAD + (uint64_t)U * TB * c->tables.maxsyms_seg + 48 + 127) & ~127ull);
+      auto lds_of = [&](size_t lut) {
+        return grouped ? tile_lds_bytes<TB_GRP, U_GRP>(lut, c->stage_bytes)
+                       : tile_lds_bytes<TB_MUL, U_MUL>(lut, c->stage_bytes) + FB_BYTES;
+      };
+      int per_cu = 0;
+      if (grouped) {
+        // compact LUT {len | sym << 24}, replicated 2^lgr times in LDS: the largest
+        // replication that keeps the best occupancy
+        const uint32_t K = c->tables.K;
+        c->tile_g = std::min<uint32_t>(4, 32 / std::max<uint32_t>(c->canon.maxlen, 1));
+        std::vector<uint32_t> lt(1u << K);
+        for (uint32_t i = 0; i < (1u << K); ++i) lt[i] = c->tables.lut2[i].x | c->tables.lut2[i].y;
+        GH_HIP(hipMalloc(&c->d_lut_t, 4ull << K));
+        GH_HIP(hipMemcpy(c->d_lut_t, lt.data(), 4ull << K, hipMemcpyHostToDevice));
+        const char* envr = getenv("GH_LGR");
+        int lg = envr ? std::clamp(atoi(envr), 0, 14 - (int)K) : std::min(5, 14 - (int)K);
+        int best = 0, best_lg = 0;
+        for (int l2 = lg; l2 >= 0; --l2) {
+          int pc = 0;
+          GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, tile_kernel_for(c->tile_path, c->tile_g),
+                                                              TB, lds_of(4ull << (K + l2))));
+          if (pc > best) { best = pc; best_lg = l2; }
+          if (envr) break;
+        }
+        c->lgr = (uint32_t)best_lg;
+        per_cu = best;
+        c->lut_bytes = 4ull << (K + best_lg);
+      } else {
+        // multi-symbol u64 LUT {syms, meta}, one copy; a narrower table if the
+        // staging leaves too little LDS (tried on a copy: the split kernels keep
+        // the loaded tables if the tile kernel does not fit at all)
+        Tables tt = c->tables;
+        while (tt.K > 6 && lds_of(8ull << tt.K) > 160 * 1024) {
+          rc = build_tables(c->canon, tt, (int)tt.K - 1, 2);
+          if (rc) return rc;
+        }
+        const size_t lb = 8ull << tt.K;
+        const int path = tt.needs_fb ? TP_MULTI_FB : TP_MULTI;
+        GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tile_kernel_for(path, 0), TB, lds_of(lb)));
+        if (per_cu >= 1) {
+          c->tables = tt;
+          c->tile_path = path;
+          GH_HIP(hipMalloc(&c->d_lut_t, lb));
+          GH_HIP(hipMemcpy(c->d_lut_t, c->tables.lut.data(), lb, hipMemcpyHostToDevice));
+          GH_HIP(hipMemcpy(c->d_fb, c->tables.fb, sizeof(c->tables.fb), hipMemcpyHostToDevice));
+        }
+        c->lgr = 0;
+        c->lut_bytes = lb;
       }
-      lg = best_lg;
-      per_cu = best;
-      c->lut_bytes = 4ull << (K + lg);
-      c->lds = tile_lds_bytes(c->lut_bytes, c->stage_bytes);
-      if (per_cu < 1) return fail(GH_E_HIP, "tile decode kernel does not fit on a CU");
-      c->lgr = (uint32_t)lg;
-      c->super = 1;
-      c->grid = (uint32_t)std::min<uint64_t>(c->ntiles, (uint64_t)per_cu * c->num_cu);
+      c->lds = lds_of(c->lut_bytes);
+      if (per_cu >= 1) {
+        c->grid = (uint32_t)std::min<uint64_t>(c->ntiles, (uint64_t)per_cu * c->num_cu);
+      } else {  // e.g. 1-2 bit codes: the staging does not fit; use the split kernels
+        c->tile = false;
+        (void)hipFree(c->d_lut_t);
+        c->d_lut_t = nullptr;
+        c->split = true;
+      }
     }
     if (c->split) {
       // split mode: tiles of U*256 segments, U = 2 (single-symbol) or 1/2 (multi)
@@ -2367,6 +2531,9 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     t.payload = c->d_payload;
     t.gaps = c->d_gaps;
     t.lut = c->d_lut_t;
+    t.fb = c->d_fb;
+    t.fb_lo = c->tables.fb_lo;
+    t.fb_hi = c->tables.fb_hi;
     t.out = c->d_out;
     t.granules = c->d_gran;
     t.plocal = c->d_gran + c->ntiles;
@@ -2390,7 +2557,8 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     static thread_local TileParams tp;
     tp = t;
     ta[0] = &tp;
-    GH_HIP(hipLaunchKernel(tile_kernel_for(c->tile_g), dim3(c->grid), dim3(TB_T), ta, c->lds, st));
+    GH_HIP(hipLaunchKernel(tile_kernel_for(c->tile_path, c->tile_g), dim3(c->grid), dim3(c->tb), ta, c->lds,
+                           st));
   } else if (c->split) {
     const SplitKernels k = split_for(c->tables.single, c->tables.needs_fb, (int)c->super,
                                      c->tables.g);
