@@ -298,12 +298,16 @@ __device__ __forceinline__ void emit_segments(Win (&v)[U], const int (&start)[U]
   }
 }
 
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t t = __shfl_up(v, d, 64);
-    if (lane >= d) v += t;
-  }
+// Inclusive wave scan on the VALU with DPP: row_shr 1/2/4/8 scans each 16-lane row,
+// row_bcast 15/31 carry the row totals forward (no LDS traffic, unlike
+// ds_bpermute-based shuffles).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int /*lane*/) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);
   return v;
 }
 
@@ -1841,6 +1845,8 @@ void gh_tile_kernel(const TileParams p) {
   STAMP_FLUSH;
 }
 
+#include "gh_msplit.hip"
+
 // ============================================================================
 // Host side
 // ============================================================================
@@ -2064,6 +2070,11 @@ struct gh_ctx {
   uint32_t lgr = 0;        // tile mode: log2 of the LUT replication
   uint32_t* d_lut_t = nullptr;  // tile mode: compact u32 LUT
   bool split = true;       // split mode (count / scan / write) vs the fused persistent kernel
+  bool ms = false;         // lean multi-symbol split kernels (gh_msplit.hip)
+  uint32_t ms_k = 0;       // their LUT width
+  uint32_t ms_last_end = 0;  // end bit of the stream's last segment when the shard holds it
+  uint2* d_ms_lut_c = nullptr;  // count LUT {b, end mask}
+  uint2* d_ms_lut_w = nullptr;  // write LUT {symbols, b | n << 8}
   uint32_t count_per = 1;  // split mode: count workgroups per write workgroup
   size_t lds_count = 0;    // split mode: dynamic LDS of the count / write kernels
   uint8_t* d_seg_cnt = nullptr;
@@ -2114,6 +2125,11 @@ static void free_shard(gh_ctx* c) {
   (void)hipFree(c->d_tile_off);
   (void)hipFree(c->d_wg_tot);
   (void)hipFree(c->d_lut_t);
+  (void)hipFree(c->d_ms_lut_c);
+  (void)hipFree(c->d_ms_lut_w);
+  c->d_ms_lut_c = nullptr;
+  c->d_ms_lut_w = nullptr;
+  c->ms = false;
   c->d_lut_t = nullptr;
   c->d_wg_tot = nullptr;
   c->d_seg_cnt = nullptr;
@@ -2127,6 +2143,94 @@ static void free_shard(gh_ctx* c) {
   c->d_lut = nullptr;
   c->d_fb = nullptr;
   c->loaded = false;
+}
+
+// Lean multi-symbol split kernels: LUTs, geometry, buffers (gh_msplit.hip).
+// Entry i of the K-bit LUTs decodes, greedily, up to four codewords lying wholly in
+// the K bits i: count LUT {b = their bits, end mask (bit e-1 per codeword end e)},
+// write LUT {their symbols (byte k = k-th), b | n << 8}.  Requires a complete code
+// with maxlen <= K, so every entry holds at least one codeword.
+static int ms_setup(gh_ctx* c) {
+  const Canon& cn = c->canon;
+  const char* ek = getenv("GH_MS_K");
+  const uint32_t K = (uint32_t)std::clamp(ek ? atoi(ek) : 12, (int)std::max<uint32_t>(cn.maxlen, 2), 12);
+  std::vector<uint2> lc(1u << K), lw(1u << K);
+  for (uint32_t i = 0; i < (1u << K); ++i) {
+    const uint32_t bits = i << (32 - K);
+    uint32_t pos = 0, n = 0, syms = 0, mask = 0;
+    while (n < 4 && pos < K) {
+      uint32_t fi = 0;
+      const uint32_t l = canon_decode16(cn, (bits << pos) >> 16, &fi);
+      if (l == 0 || pos + l > K) break;
+      syms |= (uint32_t)cn.sym[fi] << (8 * n);
+      ++n;
+      pos += l;
+      mask |= 1u << (pos - 1);
+    }
+    if (n == 0) return fail(GH_E_TABLE, "msplit: LUT entry without a codeword");
+    lc[i] = make_uint2(pos, mask);
+    lw[i] = make_uint2(syms, pos | (n << 8));
+  }
+  const size_t lb = 8ull << K;  // >= 32 bytes: whole 16-byte chunks
+  GH_HIP(hipMalloc(&c->d_ms_lut_c, lb));
+  GH_HIP(hipMalloc(&c->d_ms_lut_w, lb));
+  GH_HIP(hipMemcpy(c->d_ms_lut_c, lc.data(), lb, hipMemcpyHostToDevice));
+  GH_HIP(hipMemcpy(c->d_ms_lut_w, lw.data(), lb, hipMemcpyHostToDevice));
+  c->ms_k = K;
+  c->lut_bytes = lb;
+  c->tb = TB_MS;
+  c->super = U_MS;
+  c->ntiles = (uint32_t)ceil_div(c->nseg, (uint64_t)U_MS * TB_MS);
+  // codewords per segment: wholly inside [start, E), E - start <= 143
+  const uint32_t maxsyms = std::min<uint32_t>(143 / std::max<uint32_t>(cn.minlen, 1) + 1, 255);
+  c->stage_bytes = (uint32_t)((16 + 16 + (uint64_t)U_MS * TB_MS * maxsyms + 64 + 15) & ~15ull);
+  constexpr int NW = TB_MS / 64;
+  c->lds = lb + c->stage_bytes + 4 * (U_MS * NW + 2) + 8 * NW;
+  c->lds_count = std::max<size_t>(lb, 64);
+  int pc_c = 0, pc_w = 0;
+  GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc_c, (const void*)gh_ms_count_kernel<U_MS, TB_MS>,
+                                                      TB_MS, c->lds_count));
+  GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc_w, (const void*)gh_ms_write_kernel<U_MS, TB_MS>,
+                                                      TB_MS, c->lds));
+  if (pc_c < 1 || pc_w < 1) return fail(GH_E_HIP, "msplit kernels do not fit on a CU");
+  c->grid = (uint32_t)std::min<uint64_t>(c->ntiles, (uint64_t)pc_w * c->num_cu);
+  // count ranges nest in write ranges (floor(b*n/grid) boundaries coincide for
+  // grid_c = k*grid_w)
+  const uint32_t kk = std::max(1, pc_c / pc_w);
+  c->count_per = 1;
+  for (uint32_t k2 = kk; k2 >= 1; --k2)
+    if ((uint64_t)k2 * c->grid <= c->ntiles) { c->count_per = k2; break; }
+  GH_HIP(hipMalloc(&c->d_seg_cnt, c->nseg + 16));
+  GH_HIP(hipMalloc(&c->d_wg_tot, 8ull * c->grid * c->count_per + 16));
+  c->ms = true;
+  c->split = false;
+  c->tile = false;
+  return GH_OK;
+}
+
+// End bit of the stream's last segment (segment-relative) under the reference rule
+// "codewords starting before bit 128" (decoder.cu:529-569), its zero padding
+// decoded like the reference's: the end of the last codeword starting before 128.
+static uint32_t last_segment_end(const Canon& cn, const uint32_t* w5, uint32_t start) {
+  uint32_t pos = start;
+  while (pos < 128) {
+    const uint32_t wi = pos >> 5, sh = pos & 31;
+    const uint32_t hi = w5[wi], lo = wi + 1 < 5 ? w5[wi + 1] : 0u;
+    const uint32_t w32 = sh ? (hi << sh) | (lo >> (32 - sh)) : hi;
+    uint32_t fi = 0;
+    const uint32_t l = canon_decode16(cn, w32 >> 16, &fi);
+    if (l == 0) break;
+    pos += l;
+  }
+  return std::max<uint32_t>(pos, 128);
+}
+
+// Start bit of global segment i (i >= 1) from the host gap words.
+static uint32_t seg_start_host(const gh_stream* s, uint64_t i) {
+  const uint64_t nib = i - 1;
+  uint32_t wv;
+  std::memcpy(&wv, (const uint8_t*)s->gap_words + 4 * (nib >> 3), 4);
+  return (wv >> (4 * (nib & 7))) & 15u;
 }
 
 extern "C" int gh_device_count(void) {
@@ -2330,7 +2434,22 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
         c->split = true;
       }
     }
-    if (c->split) {
+    // Lean multi-symbol split kernels: multi-symbol codes that are complete and fit
+    // 12 bits (GH_MODE=split / fused / tile keep the older kernels).
+    {
+      uint64_t kraft = 0;
+      for (uint32_t l = 1; l <= 16; ++l) kraft += (uint64_t)c->canon.count[l] << (16 - l);
+      const bool eligible = kraft == 65536 && c->canon.maxlen <= 12 && c->canon.nsyms >= 2 &&
+                            c->nseg < (1ull << 31);
+      const bool want = envm ? !strcmp(envm, "msplit") : (!c->tables.single && c->tables.g == 0);
+        if (eligible && want) {
+        rc = ms_setup(c);
+        if (rc) return rc;
+      } else if (envm && !strcmp(envm, "msplit")) {
+        c->split = true;  // not eligible: the older split kernels
+      }
+    }
+    if (c->split && !c->ms) {
       // split mode: tiles of U*256 segments, U = 2 (single-symbol) or 1/2 (multi)
       if (c->tables.single || c->tables.g > 0) uv = 2;
       else if (!(envu && atoi(envu) == 2)) uv = (2u * TB_S * c->tables.maxsyms_seg <= 16384) ? 2 : 1;
@@ -2359,8 +2478,8 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
       GH_HIP(hipMalloc(&c->d_tile_cnt, 4ull * c->ntiles + 16));
       GH_HIP(hipMalloc(&c->d_wg_tot, 8ull * c->grid * c->count_per + 16));
     }
-    if (!c->tile) c->tb = c->split ? TB_S : c->tables.g > 0 ? TB_G : TB;
-    for (; !c->split && !c->tile; uv >>= 1) {  // fall back to a narrower ILP width if the kernel does not fit
+    if (!c->tile && !c->ms) c->tb = c->split ? TB_S : c->tables.g > 0 ? TB_G : TB;
+    for (; !c->split && !c->tile && !c->ms; uv >>= 1) {  // fall back to a narrower ILP width if the kernel does not fit
       c->super = (uint32_t)uv;
       c->stage_bytes = (uint32_t)(((uint64_t)uv * c->tb * c->tables.maxsyms_seg + 64 + 15) & ~15ull);
       c->lds = lut_bytes + FB_BYTES + 2 * c->stage_bytes + SCRATCH_BYTES;
@@ -2415,9 +2534,9 @@ extern "C" int gh_ctx_load(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e
   if (have)
     GH_HIP(hipMemcpy(c->d_payload, (const uint8_t*)s->payload + 4 * w0, 4 * have,
                      hipMemcpyHostToDevice));
-  // gap nibbles for local segments 1..nseg-1: global nibbles [b, e-1)
+  // gap nibbles: starts of local segments 1..nseg-1 and ends of all: global [b-1, e)
   const uint64_t gw0 = b >> 3;
-  const uint64_t gw1 = (e >= 2) ? ((e - 2) >> 3) + 1 : gw0 + 1;
+  const uint64_t gw1 = (e >= 1) ? ((e - 1) >> 3) + 1 : gw0 + 1;
   const uint64_t gwords = std::max<uint64_t>(gw1, gw0 + 1) - gw0;
   const uint64_t total_gw = ceil_div(s->g, GH_GAPS_PER_WORD);
   const uint64_t gcopy = (gw0 < total_gw) ? std::min<uint64_t>(gwords, total_gw - gw0) : 0;
@@ -2427,6 +2546,13 @@ extern "C" int gh_ctx_load(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e
     GH_HIP(hipMemcpy(c->d_gaps, (const uint8_t*)s->gap_words + 4 * gw0, 4 * gcopy,
                      hipMemcpyHostToDevice));
   c->gap_nib0 = (uint32_t)(b - 8 * gw0);
+  c->ms_last_end = 0;
+  if (c->ms && e == s->g) {
+    uint32_t w5[5] = {};
+    for (uint64_t i = 0; i < 5; ++i)
+      if (4 * (e - 1) + i < s->w) std::memcpy(&w5[i], (const uint8_t*)s->payload + 4 * (4 * (e - 1) + i), 4);
+    c->ms_last_end = last_segment_end(c->canon, w5, c->nseg == 1 ? c->first_start : seg_start_host(s, e - 1));
+  }
   c->loaded = true;
   return GH_OK;
 }
@@ -2449,7 +2575,7 @@ extern "C" int gh_ctx_load_device(gh_ctx* c, const gh_stream* s, uint64_t b, uin
   if (have)
     GH_HIP(hipMemcpy(c->d_payload, d_payload, 4 * have, hipMemcpyDeviceToDevice));
   const uint64_t gw0 = b >> 3;
-  const uint64_t gw1 = (e >= 2) ? ((e - 2) >> 3) + 1 : gw0 + 1;
+  const uint64_t gw1 = (e >= 1) ? ((e - 1) >> 3) + 1 : gw0 + 1;
   const uint64_t gwords = std::max<uint64_t>(gw1, gw0 + 1) - gw0;
   const uint64_t total_gw = ceil_div(s->g, GH_GAPS_PER_WORD);
   const uint64_t gcopy = (gw0 < total_gw) ? std::min<uint64_t>(gwords, total_gw - gw0) : 0;
@@ -2465,6 +2591,21 @@ extern "C" int gh_ctx_load_device(gh_ctx* c, const gh_stream* s, uint64_t b, uin
     uint32_t wv = 0;
     GH_HIP(hipMemcpy(&wv, d_gap_words + (nib >> 3), 4, hipMemcpyDeviceToHost));
     c->first_start = (wv >> (4 * (nib & 7))) & 15u;
+  }
+  c->ms_last_end = 0;
+  if (c->ms && e == s->g) {
+    uint32_t w5[5] = {};
+    const uint64_t lw0 = 4 * (c->nseg - 1);  // local word of the last segment
+    const uint64_t nw = std::min<uint64_t>(5, have > lw0 ? have - lw0 : 0);
+    if (nw) GH_HIP(hipMemcpy(w5, c->d_payload + lw0, 4 * nw, hipMemcpyDeviceToHost));
+    uint32_t st = c->first_start;
+    if (c->nseg > 1) {
+      const uint64_t nib = e - 2;
+      uint32_t wv = 0;
+      GH_HIP(hipMemcpy(&wv, d_gap_words + (nib >> 3), 4, hipMemcpyDeviceToHost));
+      st = (wv >> (4 * (nib & 7))) & 15u;
+    }
+    c->ms_last_end = last_segment_end(c->canon, w5, st);
   }
   c->loaded = true;
   return GH_OK;
@@ -2526,7 +2667,40 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
   p.tile_cnt = c->d_tile_cnt;
   p.tile_off = c->d_tile_off;
   p.wg_tot = c->d_wg_tot;
-  if (c->tile) {
+  if (c->ms) {
+    MsParams m{};
+    m.payload = c->d_payload;
+    m.gaps = c->d_gaps;
+    m.seg_cnt = c->d_seg_cnt;
+    m.wg_tot = c->d_wg_tot;
+    m.out = c->d_out;
+    m.status = c->d_misc + 1;
+    m.total = (unsigned long long*)(c->d_misc + 2);
+    m.out_cap = c->out_cap;
+    m.nseg = (uint32_t)c->nseg;
+    m.ntiles = c->ntiles;
+    m.gap_nib0 = c->gap_nib0;
+    m.first_start = c->first_start;
+    m.kbits = c->ms_k;
+    m.lut_bytes = (uint32_t)c->lut_bytes;
+    m.stage_bytes = c->stage_bytes;
+    m.count_per = c->count_per;
+    m.last_end = c->ms_last_end;
+    m.ablate = p.ablate;
+    static thread_local MsParams mc, mw;
+    static thread_local void* ac[1];
+    static thread_local void* aw[1];
+    mc = m;
+    mc.lut = c->d_ms_lut_c;
+    mw = m;
+    mw.lut = c->d_ms_lut_w;
+    ac[0] = &mc;
+    aw[0] = &mw;
+    GH_HIP(hipLaunchKernel((const void*)gh_ms_count_kernel<U_MS, TB_MS>, dim3(c->grid * c->count_per),
+                           dim3(TB_MS), ac, c->lds_count, st));
+    GH_HIP(hipLaunchKernel((const void*)gh_ms_write_kernel<U_MS, TB_MS>, dim3(c->grid), dim3(TB_MS), aw,
+                           c->lds, st));
+  } else if (c->tile) {
     TileParams t{};
     t.payload = c->d_payload;
     t.gaps = c->d_gaps;
@@ -2604,9 +2778,11 @@ extern "C" int gh_ctx_report(gh_ctx* c, void* hip_stream, gh_report* rep) {
     rep->lut_bits = c->tables.K;
     rep->grid = c->grid;
     rep->tiles = c->ntiles;
-    rep->mode = c->tile ? GH_MODE_TILE : c->split ? GH_MODE_SPLIT : GH_MODE_FUSED;
+    rep->mode = c->tile ? GH_MODE_TILE : (c->split || c->ms) ? GH_MODE_SPLIT : GH_MODE_FUSED;
     std::memcpy(&rep->slow_lookbacks, misc + 4, 8);
-    rep->path = c->tables.g > 0 ? GH_PATH_GROUPED : c->tables.single ? GH_PATH_SINGLE : GH_PATH_MULTI;
+    rep->path = c->ms ? GH_PATH_MULTI_LEAN
+                : c->tables.g > 0 ? GH_PATH_GROUPED : c->tables.single ? GH_PATH_SINGLE : GH_PATH_MULTI;
+    if (c->ms) rep->lut_bits = c->ms_k;
     rep->launches = c->nlaunch;
     rep->kernel_ms = c->nlaunch ? (float)(c->acc_ms / c->nlaunch) : 0.f;
   }

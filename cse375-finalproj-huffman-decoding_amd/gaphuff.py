@@ -86,7 +86,7 @@ class gh_report(ctypes.Structure):
 
 
 MODE_NAMES = {0: "fused", 1: "split", 2: "tile"}
-PATH_NAMES = {0: "multi", 1: "single", 2: "grouped"}
+PATH_NAMES = {0: "multi", 1: "single", 2: "grouped", 3: "multi_lean"}
 
 
 class gh_opts(ctypes.Structure):
