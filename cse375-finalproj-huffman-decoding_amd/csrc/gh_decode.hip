@@ -1231,6 +1231,9 @@ __global__ __launch_bounds__(TBK) void gh_write_kernel(const DecodeParams p) {
 // two VALU ops.  Reference counterpart: gpu_dec_l1_l2 (decoder.cu:454-730).
 // ============================================================================
 constexpr int STAGE_PAD = 16;  // staging byte STAGE_PAD + i = tile byte i
+#ifndef GH_TILE_LAG3
+#define GH_TILE_LAG3 0         // grouped path: copy out at lag 3 (measured no faster than lag 2)
+#endif
 #ifndef GH_LB_MIDG
 #define GH_LB_MIDG 2           // decode group after which the round leader loads aggregates
 #endif
@@ -1417,6 +1420,33 @@ __device__ __forceinline__ void stage_unaligned(const uint32_t (&ow)[OW], uint32
     if (t > 1) lds_st8(q + 1, x >> 8);
     if (t > 2) lds_st8(q + 2, x >> 16);
   }
+}
+
+// Aligned staging of a segment's n bytes (ow, byte 0 first) at LDS byte address o.
+// Phase 1 writes the aligned dwords holding the segment's bytes except the first
+// one when o is unaligned (zeros stand in for the next segment's bytes in its last
+// dword); phase 2, after a workgroup barrier, ORs the segment's head bytes into that
+// first dword, which by then holds the previous segment's tail (written whole by
+// it in phase 1).  Every LDS store is aligned: unaligned ds_write_b32 measured about
+// 3x the LDS time of aligned ones with per-lane offsets like these.
+// Returns the phase-2 dword (0 when o is aligned) and sets *head_addr.
+__device__ __forceinline__ uint32_t stage_aligned_p1(const uint32_t (&ow)[OW], uint32_t n, uint32_t o,
+                                                     uint32_t* head_addr) {
+  const uint32_t ap = ((o - 1u) & 3u) + 1u;  // 1..4: bytes from the dword base to o
+  const uint32_t base = o - ap;              // dword m at base + 4m holds segment bytes [4m - ap, +4)
+  const uint32_t s = 4u - ap;                // alignbyte amount
+  const uint32_t last = (n + ap - 1u) >> 2;  // last dword touched (>= 2 for n >= 7)
+#pragma unroll
+  for (int m = 1; m <= OW; ++m) {
+    const uint32_t hi = m < OW ? ow[m] : 0u;
+    const uint32_t r = __builtin_amdgcn_alignbyte(hi, ow[m - 1], s);
+    if ((uint32_t)m <= last) lds_st32(base + 4u * m, r);
+  }
+  *head_addr = base;
+  return ap < 4u ? __builtin_amdgcn_alignbyte(ow[0], 0u, s) : 0u;
+}
+__device__ __forceinline__ void lds_or32(uint32_t byte_addr, uint32_t v) {
+  asm volatile("ds_or_b32 %0, %1" :: "v"(byte_addr), "v"(v) : "memory");
 }
 
 // ---- multi-symbol path ------------------------------------------------------------
@@ -1643,31 +1673,35 @@ void gh_tile_kernel(const TileParams p) {
   };
   load(cur);
   if (cur >= p.ntiles) cur = NONE;
-  uint32_t t1 = NONE, t2 = NONE;  // tiles of iterations k-1 and k-2
-  uint32_t tot1 = 0, tot2 = 0;    // their totals
-  uint32_t buf = 0;               // staging buffer of iteration k's tile (and of k-2's)
+  // Grouped path: a tile's bytes stay in registers for one iteration, are staged in
+  // the next and copied out two iterations later (lag 3: two iterations of slack for
+  // its prefix); multi path: staged at once (emit pass), copied out at lag 2.
+  constexpr bool LAG3 = GH_TILE_LAG3 && !MULTI;
+  uint32_t t1 = NONE, t2 = NONE, t3 = NONE;  // tiles of iterations k-1, k-2, k-3
+  uint32_t tot1 = 0, tot2 = 0, tot3 = 0;     // their totals
+  uint32_t buf = 0;               // k & 1
+  uint32_t pow[LAG3 ? U : 1][LAG3 ? OW : 1], pcnt[U], pbpos[U];  // grouped: tile k-1, held
+#pragma unroll
+  for (int u = 0; u < U; ++u) pcnt[u] = 0;
   for (uint32_t k = 0;; ++k) {
     const bool have_cur = cur < p.ntiles;
-    const bool have2 = t2 < p.ntiles;
+    const uint32_t tx = LAG3 ? t3 : t2;  // the tile copied out this iteration
+    const bool have2 = tx < p.ntiles;
     // the workgroup that decoded tile rG + (r mod n_r) leads round r (n_r tiles) one
     // iteration later: every round, the last partial one included, has a leader
     const uint32_t lr = t1 < p.ntiles ? t1 / G : NONE;
     const bool lead = lr != NONE && t1 % G == lr % min(G, p.ntiles - lr * G);
-    if (!have_cur && t1 >= p.ntiles && !have2) break;
-    if (last_tile_k != NONE && k > last_tile_k + 3) {  // cannot happen; never hang the GPU
+    if (!have_cur && t1 >= p.ntiles && t2 >= p.ntiles && !have2) break;
+    if (last_tile_k != NONE && k > last_tile_k + 4) {  // cannot happen; never hang the GPU
       if (tid == 0) atomicOr(p.status, (unsigned)GH_ST_TIMEOUT);
       break;
     }
     const uint32_t par = k & 1u;
     STAMP(9);
     // prefix of tile k-2: R[round] + plocal[tile], read by lane 0 of every wave
+    // (loaded mid-decode: a load issued at the top often saw the value a little
+    // before it was published, and the re-poll then paid a full memory round trip)
     unsigned long long gr = 0, gp = 0;
-    if (have2 && lane == 0) {
-      const uint32_t r2 = t2 / G;
-      gp = __hip_atomic_load(&p.plocal[t2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      gr = r2 == 0 ? 0ull
-                   : __hip_atomic_load(&p.rprefix[r2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
     unsigned long long rl = 0;  // leader: R[lr] (wave 0 lane 0)
     if (lead && tid == 0 && lr > 0)
       rl = __hip_atomic_load(&p.rprefix[lr], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1676,6 +1710,12 @@ void gh_tile_kernel(const TileParams p) {
     const bool lvalid = lead && lt < min(p.ntiles, (lr + 1) * G);
     unsigned long long la = 0;
     auto mid = [&]() {
+      if (have2 && lane == 0) {
+        const uint32_t r2 = tx / G;
+        gp = __hip_atomic_load(&p.plocal[tx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        gr = r2 == 0 ? 0ull
+                     : __hip_atomic_load(&p.rprefix[r2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       if (lead) la = __hip_atomic_load(&p.granules[lvalid ? lt : 0], __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
     };
@@ -1742,22 +1782,24 @@ void gh_tile_kernel(const TileParams p) {
     if (have2) {
       unsigned long long goff = 0;
       if (lane == 0) {
-        const uint32_t r2 = t2 / G;
+        const uint32_t r2 = tx / G;
         if (!granule_ok(p, gp, 2)) {
           if (p.stats && wid == 0) atomicAdd(p.stats, 1ull);
-          gp = poll_granule(p, &p.plocal[t2], 2);
+          gp = poll_granule(p, &p.plocal[tx], 2);
         }
         if (r2 > 0 && !granule_ok(p, gr, 2)) {
           if (p.stats && wid == 0) atomicAdd(p.stats + 1, 1ull);
           gr = poll_granule(p, &p.rprefix[r2], 2);
         }
         goff = (gp & VMASK) + (r2 > 0 ? (gr & VMASK) : 0ull);
-        if (wid == 0 && t2 == p.ntiles - 1) *p.total = goff + tot2;
+        if (wid == 0 && tx == p.ntiles - 1) *p.total = goff + (LAG3 ? tot3 : tot2);
       }
       goff = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(goff >> 32)) << 32) |
              __builtin_amdgcn_readfirstlane((uint32_t)goff);
-      const uint32_t n2 = goff >= p.out_cap ? 0u : (uint32_t)min<unsigned long long>(tot2, p.out_cap - goff);
-      if (!ABLATE(2)) copy_out_tile<TB>(p.out, s_stage + buf * p.stage_bytes, goff, n2, tid);
+      STAMP(6);
+      const uint32_t n2 =
+          goff >= p.out_cap ? 0u : (uint32_t)min<unsigned long long>(LAG3 ? tot3 : tot2, p.out_cap - goff);
+      if (!ABLATE(2)) copy_out_tile<TB>(p.out, s_stage + (LAG3 ? buf ^ 1u : buf) * p.stage_bytes, goff, n2, tid);
     }
     STAMP(1);
     uint32_t bpos[U];
@@ -1819,20 +1861,45 @@ void gh_tile_kernel(const TileParams p) {
       }
     }
     STAMP(4);
-    if (have_cur && !ABLATE(4)) {
-      // absolute LDS address of this tile's staging (the kernel's LDS starts at 0)
-      const uint32_t sbase = p.lut_bytes + buf * p.stage_bytes + STAGE_PAD;
+    if ((LAG3 ? t1 < p.ntiles : have_cur) && !ABLATE(4)) {
+      // absolute LDS address of the staging (the kernel's LDS starts at 0): this
+      // tile's (multi), the tile of iteration k-1 (grouped)
+      const uint32_t sbase = p.lut_bytes + (LAG3 ? buf ^ 1u : buf) * p.stage_bytes + STAGE_PAD;
+      if constexpr (MULTI) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if constexpr (MULTI) {
+        for (int u = 0; u < U; ++u)
           emit_chain<FB>(make_win(mw[u], mw4[u], mstart[u]), mstart[u], mact[u], cnt[u], sbase + bpos[u],
                          kshift, p, s_fb);
-        } else {
-          stage_unaligned(ow[MULTI ? 0 : u], cnt[u], sbase + bpos[u]);
+      } else {
+        uint32_t hv[U], ha[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          hv[u] = 0;
+          ha[u] = 0;
+          if constexpr (LAG3) {
+            if (pcnt[u]) hv[u] = stage_aligned_p1(pow[u], pcnt[u], sbase + pbpos[u], &ha[u]);
+          } else {
+            if (cnt[u]) hv[u] = stage_aligned_p1(ow[u], cnt[u], sbase + bpos[u], &ha[u]);
+          }
         }
+        __syncthreads();  // phase 1 done: every segment's tail dword is in place
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (hv[u]) lds_or32(ha[u], hv[u]);
       }
     }
     STAMP(5);
+    if constexpr (LAG3) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        pcnt[u] = have_cur ? cnt[u] : 0u;
+        pbpos[u] = bpos[u];
+#pragma unroll
+        for (int m = 0; m < OW; ++m) pow[u][m] = ow[MULTI ? 0 : u][MULTI ? 0 : m];
+      }
+    }
+    t3 = t2;
+    tot3 = tot2;
     t2 = t1;
     tot2 = tot1;
     t1 = have_cur ? cur : NONE;
@@ -2145,6 +2212,19 @@ static void free_shard(gh_ctx* c) {
   c->loaded = false;
 }
 
+struct MsKernels {
+  const void* count;
+  const void* write;
+};
+template <int GL>
+static MsKernels ms_pair() {
+  return {(const void*)gh_ms_count_kernel<U_MS, TB_MS, GL>, (const void*)gh_ms_write_kernel<U_MS, TB_MS, GL>};
+}
+static MsKernels ms_kernels(uint32_t K) {
+  const int g = ms_group(K);
+  return g >= 4 ? ms_pair<4>() : g == 3 ? ms_pair<3>() : ms_pair<2>();
+}
+
 // Lean multi-symbol split kernels: LUTs, geometry, buffers (gh_msplit.hip).
 // Entry i of the K-bit LUTs decodes, greedily, up to four codewords lying wholly in
 // the K bits i: count LUT {b = their bits, end mask (bit e-1 per codeword end e)},
@@ -2153,7 +2233,7 @@ static void free_shard(gh_ctx* c) {
 static int ms_setup(gh_ctx* c) {
   const Canon& cn = c->canon;
   const char* ek = getenv("GH_MS_K");
-  const uint32_t K = (uint32_t)std::clamp(ek ? atoi(ek) : 12, (int)std::max<uint32_t>(cn.maxlen, 2), 12);
+  const uint32_t K = (uint32_t)std::clamp(ek ? atoi(ek) : 10, (int)std::max<uint32_t>(cn.maxlen, 2), 12);
   std::vector<uint2> lc(1u << K), lw(1u << K);
   for (uint32_t i = 0; i < (1u << K); ++i) {
     const uint32_t bits = i << (32 - K);
@@ -2188,10 +2268,9 @@ static int ms_setup(gh_ctx* c) {
   c->lds = lb + c->stage_bytes + 4 * (U_MS * NW + 2) + 8 * NW;
   c->lds_count = std::max<size_t>(lb, 64);
   int pc_c = 0, pc_w = 0;
-  GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc_c, (const void*)gh_ms_count_kernel<U_MS, TB_MS>,
-                                                      TB_MS, c->lds_count));
-  GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc_w, (const void*)gh_ms_write_kernel<U_MS, TB_MS>,
-                                                      TB_MS, c->lds));
+  const MsKernels mk = ms_kernels(K);
+  GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc_c, mk.count, TB_MS, c->lds_count));
+  GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc_w, mk.write, TB_MS, c->lds));
   if (pc_c < 1 || pc_w < 1) return fail(GH_E_HIP, "msplit kernels do not fit on a CU");
   c->grid = (uint32_t)std::min<uint64_t>(c->ntiles, (uint64_t)pc_w * c->num_cu);
   // count ranges nest in write ranges (floor(b*n/grid) boundaries coincide for
@@ -2696,10 +2775,9 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     mw.lut = c->d_ms_lut_w;
     ac[0] = &mc;
     aw[0] = &mw;
-    GH_HIP(hipLaunchKernel((const void*)gh_ms_count_kernel<U_MS, TB_MS>, dim3(c->grid * c->count_per),
-                           dim3(TB_MS), ac, c->lds_count, st));
-    GH_HIP(hipLaunchKernel((const void*)gh_ms_write_kernel<U_MS, TB_MS>, dim3(c->grid), dim3(TB_MS), aw,
-                           c->lds, st));
+    const MsKernels mk = ms_kernels(c->ms_k);
+    GH_HIP(hipLaunchKernel(mk.count, dim3(c->grid * c->count_per), dim3(TB_MS), ac, c->lds_count, st));
+    GH_HIP(hipLaunchKernel(mk.write, dim3(c->grid), dim3(TB_MS), aw, c->lds, st));
   } else if (c->tile) {
     TileParams t{};
     t.payload = c->d_payload;

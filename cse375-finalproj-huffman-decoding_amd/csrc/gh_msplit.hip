@@ -25,8 +25,8 @@
 //          "all allowed" while more than 32 bits remain), q -= b;
 //   write: ds_write_b32 of the four symbol bytes at ptr (lanes still inside their
 //          segment), ptr += n (SDWA byte add), q -= meta (low 5 bits = b).
-// The window is the 160-bit funnel Win; up to G_MS lookups share one 32-bit window
-// before the funnel shifts (K <= 12: two lookups consume at most 24 bits).
+// The window is the 160-bit funnel Win; GL lookups share one 32-bit window before
+// the funnel shifts (GL * K <= 31 bits).
 //
 // Staging writes are aligned ds_or_b32 pairs into a zeroed buffer (the lookup's
 // four bytes shifted to the byte offset, low and high dword): unaligned
@@ -38,7 +38,8 @@
 
 constexpr int TB_MS = 256;  // workgroup size of both kernels
 constexpr int U_MS = 2;     // segments per thread (lock-step chains)
-constexpr int G_MS = 2;     // lookups per funnel shift
+// lookups per funnel shift: G * K <= 31 (template parameter GL of the kernels)
+inline int ms_group(uint32_t K) { return K <= 7 ? 4 : K <= 10 ? 3 : 2; }
 
 struct MsParams {
   const uint32_t* payload;       // local segment j owns words [4j, 4j+4); +1 look-ahead, zero padded
@@ -127,7 +128,7 @@ __device__ __forceinline__ uint32_t ms_rmask(int R) {
   return R >= 32 ? 0xFFFFFFFFu : m;
 }
 
-template <int U, int TBK>
+template <int U, int TBK, int GL>
 __global__ __launch_bounds__(TBK) void gh_ms_count_kernel(const MsParams p) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int tid = threadIdx.x;
@@ -171,7 +172,7 @@ __global__ __launch_bounds__(TBK) void gh_ms_count_kernel(const MsParams p) {
         q[u] = 32u;
       }
 #pragma unroll
-      for (int j = 0; j < G_MS; ++j) {
+      for (int j = 0; j < GL; ++j) {
         uint2 e[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -215,7 +216,7 @@ __global__ __launch_bounds__(TBK) void gh_ms_count_kernel(const MsParams p) {
   }
 }
 
-template <int U, int TBK>
+template <int U, int TBK, int GL>
 __global__ __launch_bounds__(TBK) void gh_ms_write_kernel(const MsParams p) {
   constexpr int NWAVE = TBK / 64;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -307,7 +308,7 @@ __global__ __launch_bounds__(TBK) void gh_ms_write_kernel(const MsParams p) {
 #pragma unroll
       for (int u = 0; u < U; ++u) q[u] = 32u;
 #pragma unroll
-      for (int j = 0; j < G_MS; ++j) {
+      for (int j = 0; j < GL; ++j) {
         uint2 e[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
