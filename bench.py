@@ -21,8 +21,9 @@ K steps (inputs resident in HBM).  ``roofline.achieved`` = algorithmic bytes per
 decode (compressed payload + gap words + decoded output) / the
 decode's average duration, measured with HIP events recorded by the library on the
 stream the kernels are launched on (torch's current stream).  A decode is one
-kernel (fused mode) or a count kernel followed by a write kernel (split mode);
-``roofline.mode`` says which.  ``cpu_baseline`` times
+kernel (tile mode: the persistent gh_tile_kernel) or a count kernel followed by a
+write kernel (split mode); ``roofline.mode`` / ``roofline.kernel`` say which.  For a
+two-kernel decode ``achieved`` is over the pair's combined duration.  ``cpu_baseline`` times
 the reference's own sequential.cpp (compiled from its sources into oracle/_ref by
 oracle/Makefile) on a bounded sample, rank 0 at N=1 only.
 """
@@ -51,6 +52,15 @@ WORKLOADS = {
     "cfg3": (10**9, 0.9, "configs[2]: 1 GB, redundancy=0.9 (short codes), per GPU"),
     "cfg4": (10**9, 0.1, "configs[3]: 1 GB, redundancy=0.1 (long codes), per GPU"),
     "cfg5": (10**9, 0.5, "configs[4]: 1 GB per GPU (8 GB at 8 GPUs), redundancy=0.5"),
+}
+
+
+# (mode, path) -> the kernels one decode launches (rocprofv3 names); path -1 = any
+KERNEL_NAMES = {
+    (1, 3): "gh::gh_ms_count_kernel + gh::gh_ms_write_kernel",
+    (1, -1): "gh::gh_count_kernel + gh::gh_write_kernel",
+    (2, -1): "gh::gh_tile_kernel",
+    (0, -1): "gh::gh_decode_kernel",
 }
 
 
@@ -223,8 +233,8 @@ def main() -> int:
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": traffic,
-                         "kernel": ("gh::gh_count_kernel + gh::gh_write_kernel"
-                                    if rep.mode == 1 else "gh::gh_decode_kernel"),
+                         "kernel": KERNEL_NAMES.get((int(rep.mode), int(rep.path)),
+                                                    KERNEL_NAMES.get((int(rep.mode), -1))),
                          "mode": gh.MODE_NAMES.get(int(rep.mode)),
                          "path": gh.PATH_NAMES.get(int(rep.path)),
                          "kernel_ms": round(kern_ms, 4), "max_kernel_ms_over_ranks": round(max_kern, 4),
