@@ -1231,6 +1231,9 @@ __global__ __launch_bounds__(TBK) void gh_write_kernel(const DecodeParams p) {
 // two VALU ops.  Reference counterpart: gpu_dec_l1_l2 (decoder.cu:454-730).
 // ============================================================================
 constexpr int STAGE_PAD = 16;  // staging byte STAGE_PAD + i = tile byte i
+#ifndef GH_PREFETCH_LATE
+#define GH_PREFETCH_LATE 1     // grouped path: issue the next tile's loads after the copy-out
+#endif
 #ifndef GH_TILE_LAG3
 #define GH_TILE_LAG3 0         // grouped path: copy out at lag 3 (measured no faster than lag 2)
 #endif
@@ -1329,6 +1332,10 @@ __device__ __forceinline__ void decode_tile_grouped(uint32_t (&e)[U][5], const i
     for (int k = 0; k < OW; ++k) ow[u][k] = 0;
   }
   bool mid_done = false;
+  // q counts down from 32 by whole LUT entries {len | sym << 24}: its low 24 bits stay
+  // exact, v_alignbit reads only the low 5, and the liveness test (q > T, the
+  // codeword starts before the segment end) reads the low 16 sign-extended (SDWA).
+  // Codewords past the end still go into ow: the staging never reads them.
 #pragma unroll
   for (int gi = 0; gi < NG; ++gi) {
 #pragma unroll
@@ -1344,11 +1351,11 @@ __device__ __forceinline__ void decode_tile_grouped(uint32_t (&e)[U][5], const i
         lds_wait_all(ent);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          const bool live = (int)q[u] > T[u];
-          cnt[u] = live ? (uint32_t)(pos + 1) : cnt[u];
-          const uint32_t sb = live ? ent[u] : 0u;
-          ow[u][pos >> 2] = __builtin_amdgcn_perm(sb, ow[u][pos >> 2], perm_sel(pos & 3));
-          q[u] -= ent[u] & 31u;
+          asm("v_cmp_gt_i32_sdwa vcc, sext(%1), %2 src0_sel:WORD_0 src1_sel:DWORD\n\t"
+              "v_addc_co_u32 %0, vcc, 0, %0, vcc"
+              : "+v"(cnt[u]) : "v"(q[u]), "v"(T[u]) : "vcc");
+          ow[u][pos >> 2] = __builtin_amdgcn_perm(ent[u], ow[u][pos >> 2], perm_sel(pos & 3));
+          q[u] -= ent[u];
         }
       }
     }
@@ -1360,7 +1367,7 @@ __device__ __forceinline__ void decode_tile_grouped(uint32_t (&e)[U][5], const i
       e[u][2] = __builtin_amdgcn_alignbit(e[u][2], e[u][3], q[u]);
       e[u][3] = __builtin_amdgcn_alignbit(e[u][3], e[u][4], q[u]);
       e[u][4] = __builtin_amdgcn_alignbit(e[u][4], 0u, q[u]);
-      T[u] += 32 - (int)q[u];
+      T[u] += 32 - (int)(int16_t)q[u];
       q[u] = 32;
       more |= 32 > T[u];
     }
@@ -1423,15 +1430,14 @@ __device__ __forceinline__ void stage_unaligned(const uint32_t (&ow)[OW], uint32
 }
 
 // Aligned staging of a segment's n bytes (ow, byte 0 first) at LDS byte address o.
-// Phase 1 writes the aligned dwords holding the segment's bytes except the first
-// one when o is unaligned (zeros stand in for the next segment's bytes in its last
-// dword); phase 2, after a workgroup barrier, ORs the segment's head bytes into that
-// first dword, which by then holds the previous segment's tail (written whole by
-// it in phase 1).  Every LDS store is aligned: unaligned ds_write_b32 measured about
-// 3x the LDS time of aligned ones with per-lane offsets like these.
-// Returns the phase-2 dword (0 when o is aligned) and sets *head_addr.
-__device__ __forceinline__ uint32_t stage_aligned_p1(const uint32_t (&ow)[OW], uint32_t n, uint32_t o,
-                                                     uint32_t* head_addr) {
+// Phase 1 writes the aligned dwords holding the segment's bytes, except the first
+// one when o is unaligned; its last dword carries whatever ow holds past byte n.
+// Phase 2, after a workgroup barrier, writes the segment's head bytes (the 1-3 bytes
+// of that skipped first dword) exactly, over the previous segment's phase-1 tail.
+// Every dword store is aligned: unaligned ds_write_b32 measured about 3x the LDS
+// time of aligned ones with per-lane offsets like these.
+// Returns the number of head bytes (0 when o is aligned).
+__device__ __forceinline__ uint32_t stage_aligned_p1(const uint32_t (&ow)[OW], uint32_t n, uint32_t o) {
   const uint32_t ap = ((o - 1u) & 3u) + 1u;  // 1..4: bytes from the dword base to o
   const uint32_t base = o - ap;              // dword m at base + 4m holds segment bytes [4m - ap, +4)
   const uint32_t s = 4u - ap;                // alignbyte amount
@@ -1442,11 +1448,12 @@ __device__ __forceinline__ uint32_t stage_aligned_p1(const uint32_t (&ow)[OW], u
     const uint32_t r = __builtin_amdgcn_alignbyte(hi, ow[m - 1], s);
     if ((uint32_t)m <= last) lds_st32(base + 4u * m, r);
   }
-  *head_addr = base;
-  return ap < 4u ? __builtin_amdgcn_alignbyte(ow[0], 0u, s) : 0u;
+  return 4u - ap;
 }
-__device__ __forceinline__ void lds_or32(uint32_t byte_addr, uint32_t v) {
-  asm volatile("ds_or_b32 %0, %1" :: "v"(byte_addr), "v"(v) : "memory");
+// Phase 2: the nb (1..3) head bytes h at o (o + (nb & 1) is even).
+__device__ __forceinline__ void stage_head(uint32_t o, uint32_t h, uint32_t nb) {
+  if (nb & 1u) asm volatile("ds_write_b8 %0, %1" :: "v"(o), "v"(h) : "memory");
+  if (nb & 2u) asm volatile("ds_write_b16 %0, %1" :: "v"(o + (nb & 1u)), "v"(h >> (8u * (nb & 1u))) : "memory");
 }
 
 // ---- multi-symbol path ------------------------------------------------------------
@@ -1520,7 +1527,8 @@ __device__ __forceinline__ void emit_chain(Win v, int start, bool act, uint32_t 
 // byte by the lanes that own them.
 template <int TBK>
 __device__ __forceinline__ void copy_out_tile(uint8_t* out, const uint8_t* stg,
-                                              unsigned long long goff, uint32_t n, int tid) {
+                                              unsigned long long goff, uint32_t n, int tid,
+                                              uint32_t abl = 0) {
   if (n == 0) return;
   const uint4* st4 = (const uint4*)stg;
   const uint32_t lb = (uint32_t)(goff & 15);
@@ -1556,7 +1564,7 @@ __device__ __forceinline__ void copy_out_tile(uint8_t* out, const uint8_t* stg,
     // tile bytes covered by this chunk: [16c - lb, 16c - lb + 16)
     const int r0 = (int)(16u * c) - (int)lb;
     if (r0 >= 0 && r0 + 16 <= (int)n) {
-      *(uint4*)(o + 16ull * c) = v;
+      if (!(abl & 16) || v.x == 0x9E3779B9u) *(uint4*)(o + 16ull * c) = v;
     } else {  // edge chunk: bytes [k0, k1) of it belong to the tile
       const int k0 = max(0, -r0), k1 = min(16, (int)n - r0);
       uint8_t* oc = o + 16ull * c;
@@ -1756,7 +1764,9 @@ void gh_tile_kernel(const TileParams p) {
         start[u] = seg == 0 ? (int)p.first_start : (int)((gw[u] >> (4 * nib)) & 15u);
         make_ewin(w[u], w4[u], start[u], S, e[u]);
       }
+#if !GH_PREFETCH_LATE
       load(nxt);  // prefetch the next iteration's tile
+#endif
       if (have_cur && ABLATE(8)) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -1799,9 +1809,13 @@ void gh_tile_kernel(const TileParams p) {
       STAMP(6);
       const uint32_t n2 =
           goff >= p.out_cap ? 0u : (uint32_t)min<unsigned long long>(LAG3 ? tot3 : tot2, p.out_cap - goff);
-      if (!ABLATE(2)) copy_out_tile<TB>(p.out, s_stage + (LAG3 ? buf ^ 1u : buf) * p.stage_bytes, goff, n2, tid);
+      if (!ABLATE(2)) copy_out_tile<TB>(p.out, s_stage + (LAG3 ? buf ^ 1u : buf) * p.stage_bytes, goff, n2, tid,
+                                      p.ablate);
     }
     STAMP(1);
+#if GH_PREFETCH_LATE
+    if constexpr (!MULTI) load(nxt);  // prefetch the next tile after the copy-out's waits
+#endif
     uint32_t bpos[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -1871,21 +1885,24 @@ void gh_tile_kernel(const TileParams p) {
           emit_chain<FB>(make_win(mw[u], mw4[u], mstart[u]), mstart[u], mact[u], cnt[u], sbase + bpos[u],
                          kshift, p, s_fb);
       } else {
-        uint32_t hv[U], ha[U];
+        uint32_t nb[U], hv[U], ha[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          hv[u] = 0;
-          ha[u] = 0;
+          nb[u] = 0;
           if constexpr (LAG3) {
-            if (pcnt[u]) hv[u] = stage_aligned_p1(pow[u], pcnt[u], sbase + pbpos[u], &ha[u]);
+            hv[u] = pow[u][0];
+            ha[u] = sbase + pbpos[u];
+            if (pcnt[u]) nb[u] = stage_aligned_p1(pow[u], pcnt[u], ha[u]);
           } else {
-            if (cnt[u]) hv[u] = stage_aligned_p1(ow[u], cnt[u], sbase + bpos[u], &ha[u]);
+            hv[u] = ow[u][0];
+            ha[u] = sbase + bpos[u];
+            if (cnt[u]) nb[u] = stage_aligned_p1(ow[u], cnt[u], ha[u]);
           }
         }
         __syncthreads();  // phase 1 done: every segment's tail dword is in place
 #pragma unroll
         for (int u = 0; u < U; ++u)
-          if (hv[u]) lds_or32(ha[u], hv[u]);
+          if (nb[u]) stage_head(ha[u], hv[u], nb[u]);
       }
     }
     STAMP(5);
@@ -2263,9 +2280,23 @@ static int ms_setup(gh_ctx* c) {
   c->ntiles = (uint32_t)ceil_div(c->nseg, (uint64_t)U_MS * TB_MS);
   // codewords per segment: wholly inside [start, E), E - start <= 143
   const uint32_t maxsyms = std::min<uint32_t>(143 / std::max<uint32_t>(cn.minlen, 1) + 1, 255);
-  c->stage_bytes = (uint32_t)((16 + 16 + (uint64_t)U_MS * TB_MS * maxsyms + 64 + 15) & ~15ull);
+  // Staging: the most workgroups per CU (4, 3, 2) whose staging still holds one
+  // chain's worst case (TB_MS segments x maxsyms); a tile that exceeds it is staged
+  // one chain at a time (gh_ms_write_kernel).
   constexpr int NW = TB_MS / 64;
-  c->lds = lb + c->stage_bytes + 4 * (U_MS * NW + 2) + 8 * NW;
+  const size_t misc = 4 * (U_MS * NW + 2) + 8 * NW;
+  const size_t chain_worst = (size_t)TB_MS * maxsyms + 64 + 32;
+  const size_t full_worst = (size_t)U_MS * TB_MS * maxsyms + 64 + 32;
+  size_t stage = 0;
+  for (int wg = 4; wg >= 1 && stage == 0; --wg) {
+    const long avail = (long)(163840 / wg) - (long)lb - (long)misc;
+    if (avail >= (long)chain_worst) stage = std::min<size_t>((size_t)avail & ~15ull, (full_worst + 15) & ~15ull);
+  }
+  if (stage == 0) return fail(GH_E_HIP, "msplit staging does not fit");
+  if (const char* es = getenv("GH_MS_STAGE"))  // tests: force a small staging (per-chain tiles)
+    stage = std::max<size_t>((size_t)atoll(es), (chain_worst + 15) & ~15ull) & ~15ull;
+  c->stage_bytes = (uint32_t)stage;
+  c->lds = lb + c->stage_bytes + misc;
   c->lds_count = std::max<size_t>(lb, 64);
   int pc_c = 0, pc_w = 0;
   const MsKernels mk = ms_kernels(K);

@@ -260,14 +260,20 @@ __global__ __launch_bounds__(TBK) void gh_ms_write_kernel(const MsParams p) {
   for (int q2 = 0; q2 < NWAVE; ++q2) goff += s_base[q2];
   const uint32_t stage0 = p.lut_bytes;  // absolute LDS address of the staging buffer
   for (uint32_t t = t0; t < t1; ++t) {
-    Win v[U];
+    int start[U];
     uint32_t cc[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t seg = t * (uint32_t)(U * TBK) + (uint32_t)(u * TBK + tid);
-      const int start = seg == 0 ? (int)p.first_start : (int)ms_nib(ga[u], p.gap_nib0 + seg - 1u);
-      v[u] = make_win(w[u], w4[u], start);
+      start[u] = seg == 0 ? (int)p.first_start : (int)ms_nib(ga[u], p.gap_nib0 + seg - 1u);
       cc[u] = seg < p.nseg ? c8[u] : 0u;
+    }
+    uint4 wc[U];
+    uint32_t w4c[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      wc[u] = w[u];
+      w4c[u] = w4[u];
     }
     if (t + 1 < t1) {  // prefetch the next tile
       ms_load<U, TBK>(p, t + 1, tid, w, w4, ga, gb);
@@ -282,79 +288,109 @@ __global__ __launch_bounds__(TBK) void gh_ms_write_kernel(const MsParams p) {
       bpos[u] = incl - cc[u];
     }
     __syncthreads();  // wave sums; the previous tile's copy-out is done
-    const uint32_t lb = (uint32_t)(goff & 15);
-    uint32_t ttot = 0;
+    uint32_t ttot = 0, ctot[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       uint32_t add = ttot;
+      ctot[u] = 0;
 #pragma unroll
       for (int q2 = 0; q2 < NWAVE; ++q2) {
         const uint32_t x = s_wsum[u * NWAVE + q2];
         add += (q2 < wid) ? x : 0u;
-        ttot += x;
+        ctot[u] += x;
       }
+      ttot += ctot[u];
       bpos[u] += add;
     }
-    // staging byte 16 + lb + i = tile byte i, so staging chunk c <-> output bytes
-    // [goff - lb - 16 + 16c, +16): aligned 16-byte copies
-    uint32_t ptr[U], end[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      ptr[u] = stage0 + 16u + lb + bpos[u];
-      end[u] = ptr[u] + cc[u];
-    }
-    for (int g = 0; g < 160; ++g) {
-      uint32_t q[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) q[u] = 32u;
-#pragma unroll
-      for (int j = 0; j < GL; ++j) {
-        uint2 e[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const uint32_t x = j == 0 ? v[u].d0 : __builtin_amdgcn_alignbit(v[u].d0, v[u].d1, q[u]);
-          e[u] = ms_lds_u64((x >> sh) & amask);
-        }
-        ms_wait(e);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          if (!(p.ablate & 2) && ptr[u] < end[u]) ms_lds_or_bytes(ptr[u], e[u].x);
-          ptr[u] = ms_add_n(ptr[u], e[u].y);
-          q[u] -= e[u].y;
-        }
-      }
-      bool more = false;
+    // A tile whose bytes exceed the staging (rare: the staging is sized for typical
+    // tiles so that four workgroups fit a CU) is staged one chain (TBK contiguous
+    // segments) at a time.
+    const uint32_t nh = ttot + 64u <= p.stage_bytes ? 1u : (uint32_t)U;
+    uint32_t hoff = 0;  // tile bytes before this half
+    for (uint32_t h = 0; h < nh; ++h) {
+      const uint32_t hbytes = nh == 1 ? ttot : ctot[h];
+      if (h > 0) __syncthreads();  // the previous half's copy-out is done
+      const uint32_t lb = (uint32_t)(goff & 15);
+      // staging byte 16 + lb + i = byte i of this half, so staging chunk c <-> output
+      // bytes [goff - lb - 16 + 16c, +16): aligned 16-byte copies
+      Win v[U];
+      uint32_t ptr[U], end[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        ms_shift(v[u], q[u]);
-        more |= ptr[u] < end[u];
+        const bool on = nh == 1 || (uint32_t)u == h;
+        v[u] = make_win(wc[u], w4c[u], start[u]);
+        // a chain not staged in this half gets ptr == end == 0: it never writes, and
+        // its ptr only grows (bpos - hoff would wrap below zero for chain 0 in half 1)
+        ptr[u] = on ? stage0 + 16u + lb + bpos[u] - hoff : 0u;
+        end[u] = on ? ptr[u] + cc[u] : 0u;
       }
-      if (!__any(more)) break;
-    }
-    __syncthreads();  // tile staged
-    // copy out: chunk c of the staging <-> output bytes [a0 - 16 + 16c, +16)
-    const unsigned long long a0 = goff - lb;
-    const unsigned long long oend = min(goff + ttot, p.out_cap);
-    const uint32_t nz = (16u + lb + ttot + 15u) >> 4;
-    uint4* st4 = (uint4*)s_stage;
-    // chunks [0, nz + 1): the tile's bytes plus the spill of its last segment
-    for (uint32_t c = tid; c < nz + 1u; c += TBK) {
-      const unsigned long long gs = a0 - 16 + 16ull * c;
-      const uint4 d = st4[c];
-      st4[c] = make_uint4(0, 0, 0, 0);
-      if (c == 0 || gs >= oend || (p.ablate & 4)) continue;
-      if (gs >= goff && gs + 16 <= oend) {
-        *(uint4*)(p.out + gs) = d;
-      } else {
-        const uint8_t* bb = (const uint8_t*)&d;
+      for (int g = 0; g < 160; ++g) {
+        uint32_t q[U];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          const unsigned long long ga2 = gs + k;
-          if (ga2 >= goff && ga2 < oend) p.out[ga2] = bb[k];
+        for (int u = 0; u < U; ++u) q[u] = 32u;
+#pragma unroll
+        for (int j = 0; j < GL; ++j) {
+          uint2 e[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const uint32_t x = j == 0 ? v[u].d0 : __builtin_amdgcn_alignbit(v[u].d0, v[u].d1, q[u]);
+            e[u] = ms_lds_u64((x >> sh) & amask);
+          }
+          ms_wait(e);
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            if (!(p.ablate & 2) && ptr[u] < end[u]) ms_lds_or_bytes(ptr[u], e[u].x);
+            ptr[u] = ms_add_n(ptr[u], e[u].y);
+            q[u] -= e[u].y;
+          }
+        }
+        bool more = false;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          ms_shift(v[u], q[u]);
+          more |= ptr[u] < end[u];
+        }
+        if (!__any(more)) break;
+      }
+      __syncthreads();  // staged
+      // copy out chunks [1, nz) (chunk 0 precedes the bytes), zero [0, nz + 1) (the
+      // last segment may spill past the end); four chunks per thread in flight
+      const unsigned long long a0 = goff - lb;
+      const unsigned long long oend = min(goff + hbytes, p.out_cap);
+      const uint32_t nz = (16u + lb + hbytes + 15u) >> 4;
+      uint4* st4 = (uint4*)s_stage;
+      for (uint32_t c0 = tid; c0 < nz + 1u; c0 += 4u * TBK) {
+        uint4 d[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t c = c0 + (uint32_t)i * TBK;
+          d[i] = c < nz + 1u ? st4[c] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t c = c0 + (uint32_t)i * TBK;
+          if (c < nz + 1u) st4[c] = make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t c = c0 + (uint32_t)i * TBK;
+          const unsigned long long gs = a0 - 16 + 16ull * c;
+          if (c == 0 || c >= nz + 1u || gs >= oend || (p.ablate & 4)) continue;
+          if (gs >= goff && gs + 16 <= oend) {
+            *(uint4*)(p.out + gs) = d[i];
+          } else {
+            const uint32_t wv[4] = {d[i].x, d[i].y, d[i].z, d[i].w};
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+              const unsigned long long ga2 = gs + k;
+              if (ga2 >= goff && ga2 < oend) p.out[ga2] = (uint8_t)(wv[k >> 2] >> (8 * (k & 3)));
+            }
+          }
         }
       }
+      goff += hbytes;
+      hoff += hbytes;
     }
-    goff += ttot;
   }
   if (blockIdx.x == gridDim.x - 1 && tid == 0) *p.total = goff;
 }

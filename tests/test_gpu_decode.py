@@ -220,3 +220,51 @@ def test_bench_contract_small(gpu):
 def test_graft_smoke(gpu):
     import __graft_entry__
     __graft_entry__.smoke()
+
+
+@pytest.mark.parametrize("k", ["", "10", "11", "12"])
+@pytest.mark.parametrize("stage", ["", "1"])
+def test_lean_split_widths_and_staging(gpu, orc, k, stage, monkeypatch):
+    """The lean multi-symbol split kernels (gh_msplit.hip) at every LUT width, with the
+    default staging and with the staging forced down to one chain's worst case, so
+    that tiles are staged one chain at a time (GH_MS_STAGE)."""
+    monkeypatch.setenv("GH_MODE", "msplit")
+    if k:
+        monkeypatch.setenv("GH_MS_K", k)
+    if stage:
+        monkeypatch.setenv("GH_MS_STAGE", stage)
+    for seed, r, n in ((31, 0.9, 700_001), (32, 0.5, 400_003), (33, 0.999, 65_549), (34, 0.1, 9_999)):
+        data = gpu.generate(seed, r, n)
+        img = _roundtrip(gpu, orc, data)
+        s = gpu.parse(img)
+        with gpu.Decoder(0) as d:
+            d.load(s)
+            d.decode()
+            rep = d.report()
+        if max(l for _, l in s.symbols) <= 12:
+            assert gpu.PATH_NAMES[rep.path] == "multi_lean"
+        total = sum(orc.segment_count(img, i) for i in range(s.g)) if n < 100_000 else None
+        if total is not None:
+            assert rep.symbols == total
+
+
+def test_lean_split_shard_counts(gpu, orc, monkeypatch):
+    """Shards through the lean split kernels: per-shard symbol counts equal the
+    reference segment rule's (decoder.cu:529-569), including the stream's last
+    segment (its zero padding, last_segment_end)."""
+    monkeypatch.setenv("GH_MODE", "msplit")
+    data = gpu.generate(35, 0.5, 250_000)
+    img = gpu.encode(data)
+    s = gpu.parse(img)
+    bounds = gpu.plan_shards(s.g, 4)
+    off = 0
+    for k in range(4):
+        with gpu.Decoder(0) as d:
+            d.load(s, bounds[k], bounds[k + 1])
+            d.decode()
+            r = d.report()
+            expect = sum(orc.segment_count(img, i) for i in range(bounds[k], bounds[k + 1]))
+            assert r.symbols == expect and r.status == 0
+            keep = min(r.symbols, s.n - off)
+            assert np.array_equal(d.download(keep), data[off:off + keep])
+            off += r.symbols
