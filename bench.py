@@ -58,6 +58,7 @@ WORKLOADS = {
 # (mode, path) -> the kernels one decode launches (rocprofv3 names); path -1 = any
 KERNEL_NAMES = {
     (1, 3): "gh::gh_ms_count_kernel + gh::gh_ms_write_kernel",
+    (1, 2): "gh::gh_gs_count_kernel + gh::gh_gs_write_kernel",
     (1, -1): "gh::gh_count_kernel + gh::gh_write_kernel",
     (2, -1): "gh::gh_tile_kernel",
     (0, -1): "gh::gh_decode_kernel",

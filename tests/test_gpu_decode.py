@@ -268,3 +268,22 @@ def test_lean_split_shard_counts(gpu, orc, monkeypatch):
             keep = min(r.symbols, s.n - off)
             assert np.array_equal(d.download(keep), data[off:off + keep])
             off += r.symbols
+
+
+@pytest.mark.parametrize("mode", ["gsplit", "tile"])
+def test_grouped_split_and_tile(gpu, orc, mode, monkeypatch):
+    """The grouped single-symbol codes (complete, minlen >= 4) through the tile kernel
+    and through the sync-free count/write kernels (gh_gsplit.hip): bytes and symbol
+    totals equal the oracle's (reference segment rule, decoder.cu:529-569)."""
+    monkeypatch.setenv("GH_MODE", mode)
+    for seed, n in ((41, 1_000_003), (42, 131_072), (43, 9_999)):
+        data = gpu.generate(seed, 0.1, n)
+        img = _roundtrip(gpu, orc, data)
+        s = gpu.parse(img)
+        with gpu.Decoder(0) as d:
+            d.load(s)
+            d.decode()
+            rep = d.report()
+        assert gpu.PATH_NAMES[rep.path] == "grouped" and rep.status == 0
+        if n < 200_000:
+            assert rep.symbols == sum(orc.segment_count(img, i) for i in range(s.g))
