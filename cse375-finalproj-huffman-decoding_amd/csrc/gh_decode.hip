@@ -1623,7 +1623,8 @@ template <int TB, int U, int PATH, int GRP>
 __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4)))
 void gh_tile_kernel(const TileParams p) {
   constexpr int NWAVE_T = TB / 64;
-  constexpr int LDR_NB = TB / 64;  // leader batches: one wave per 64 tiles of a round
+  constexpr int LDR_NB = TB / 64;  // leader batches: one wave per 64 * LPL tiles of a round
+  constexpr int LPL = TB >= 512 ? 1 : 1024 / TB;  // aggregates per leader lane (grid <= LPL * TB)
   constexpr bool MULTI = PATH != TP_GROUPED;
   constexpr bool FB = PATH == TP_MULTI_FB;
   static_assert(!MULTI || U == 1, "multi-symbol path: one segment per lane");
@@ -1713,10 +1714,16 @@ void gh_tile_kernel(const TileParams p) {
     unsigned long long rl = 0;  // leader: R[lr] (wave 0 lane 0)
     if (lead && tid == 0 && lr > 0)
       rl = __hip_atomic_load(&p.rprefix[lr], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // leader: the round's aggregates, one per lane (issued mid-decode)
-    const uint32_t lt = lr * G + 64u * (uint32_t)wid + (uint32_t)lane;  // tile of this lane
-    const bool lvalid = lead && lt < min(p.ntiles, (lr + 1) * G);
-    unsigned long long la = 0;
+    // leader: the round's aggregates, LPL consecutive tiles per lane (issued mid-decode)
+    const uint32_t lt = lr * G + (uint32_t)tid * LPL;  // first tile of this lane
+    const uint32_t lend = min(p.ntiles, (lr + 1) * G);
+    bool lvalid[LPL];
+    unsigned long long la[LPL];
+#pragma unroll
+    for (int j = 0; j < LPL; ++j) {
+      lvalid[j] = lead && lt + j < lend;
+      la[j] = 0;
+    }
     auto mid = [&]() {
       if (have2 && lane == 0) {
         const uint32_t r2 = tx / G;
@@ -1724,7 +1731,10 @@ void gh_tile_kernel(const TileParams p) {
         gr = r2 == 0 ? 0ull
                      : __hip_atomic_load(&p.rprefix[r2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      if (lead) la = __hip_atomic_load(&p.granules[lvalid ? lt : 0], __ATOMIC_RELAXED,
+      if (lead)
+#pragma unroll
+        for (int j = 0; j < LPL; ++j)
+          la[j] = __hip_atomic_load(&p.granules[lvalid[j] ? lt + j : 0], __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
     };
     // ---- decode this tile (its words were loaded during the previous iteration) --
@@ -1824,14 +1834,24 @@ void gh_tile_kernel(const TileParams p) {
       bpos[u] = incl - cnt[u];
     }
     // leader: every aggregate of the round published?  (rarely not: poll)
-    uint32_t lval = 0, lincl = 0;
+    uint32_t lval[LPL], lsum = 0, lincl = 0;
     if (lead) {
-      if (!__all(!lvalid || granule_ok(p, la, 1) || granule_ok(p, la, 2))) {
+      bool ready = true;
+#pragma unroll
+      for (int j = 0; j < LPL; ++j) ready &= !lvalid[j] || granule_ok(p, la[j], 1) || granule_ok(p, la[j], 2);
+      if (!__all(ready)) {
         if (lane == 0 && p.stats) atomicAdd(p.stats + 2, 1ull);
-        if (lvalid && !(granule_ok(p, la, 1) || granule_ok(p, la, 2))) la = poll_granule(p, &p.granules[lt], 1);
+#pragma unroll
+        for (int j = 0; j < LPL; ++j)
+          if (lvalid[j] && !(granule_ok(p, la[j], 1) || granule_ok(p, la[j], 2)))
+            la[j] = poll_granule(p, &p.granules[lt + j], 1);
       }
-      lval = lvalid ? (uint32_t)(la & VMASK) : 0u;  // a tile holds < 2^32 symbols
-      lincl = wave_incl_scan(lval, lane);
+#pragma unroll
+      for (int j = 0; j < LPL; ++j) {
+        lval[j] = lvalid[j] ? (uint32_t)(la[j] & VMASK) : 0u;  // a tile holds < 2^32 symbols
+        lsum += lval[j];
+      }
+      lincl = wave_incl_scan(lsum, lane);
       if (lane == 63) s_lead[wid] = lincl;
     }
     STAMP(2);
@@ -1861,9 +1881,14 @@ void gh_tile_kernel(const TileParams p) {
         before += (q < wid) ? x : 0u;
         total += x;
       }
-      if (lvalid)
-        __hip_atomic_store(&p.plocal[lt], granule(p.epoch, 2, before + lincl - lval),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      unsigned long long run = before + lincl - lsum;
+#pragma unroll
+      for (int j = 0; j < LPL; ++j) {
+        if (lvalid[j])
+          __hip_atomic_store(&p.plocal[lt + j], granule(p.epoch, 2, run), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        run += lval[j];
+      }
       if (tid == 0) {
         if (lr > 0 && !granule_ok(p, rl, 2)) {
           if (p.stats) atomicAdd(p.stats + 3, 1ull);
@@ -2138,7 +2163,10 @@ static SplitKernels split_for(bool single, bool fb, int uv, int g) {
 // Tile-mode kernel geometry: the grouped path runs 512-thread workgroups with two
 // segments per lane; the multi-symbol paths 1024-thread workgroups with one (their
 // staging is up to 64 bytes per segment).
-constexpr int TB_GRP = 512, U_GRP = 2, TB_MUL = 1024, U_MUL = 1;
+#ifndef GH_TB_GRP
+#define GH_TB_GRP 512  // grouped tile path workgroup size (256: 4 per CU, measured 1.5x slower: more stragglers per round)
+#endif
+constexpr int TB_GRP = GH_TB_GRP, U_GRP = 2, TB_MUL = 1024, U_MUL = 1;
 static const void* tile_kernel_for(int path, uint32_t g) {
   if (path == TP_MULTI) return (const void*)gh_tile_kernel<TB_MUL, U_MUL, TP_MULTI, 0>;
   if (path == TP_MULTI_FB) return (const void*)gh_tile_kernel<TB_MUL, U_MUL, TP_MULTI_FB, 0>;
@@ -2595,7 +2623,9 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
       }
       c->lds = lds_of(c->lut_bytes);
       if (per_cu >= 1) {
-        c->grid = (uint32_t)std::min<uint64_t>(c->ntiles, (uint64_t)per_cu * c->num_cu);
+        // a round's aggregates are read by its leader, LPL per lane: grid <= LPL * TB
+        const uint64_t gmax = (uint64_t)TB * (TB >= 512 ? 1 : 1024 / TB);
+        c->grid = (uint32_t)std::min<uint64_t>({(uint64_t)c->ntiles, (uint64_t)per_cu * c->num_cu, gmax});
       } else {  // e.g. 1-2 bit codes: the staging does not fit; use the split kernels
         c->tile = false;
         (void)hipFree(c->d_lut_t);
