@@ -2638,7 +2638,7 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
     {
       uint64_t kraft = 0;
       for (uint32_t l = 1; l <= 16; ++l) kraft += (uint64_t)c->canon.count[l] << (16 - l);
-      const bool eligible = kraft == 65536 && c->canon.maxlen <= 12 && c->canon.nsyms >= 2 &&
+      const bool eligible = kraft == 65536 && c->canon.maxlen <= 12 && c->canon.minlen >= 2 &&
                             c->nseg < (1ull << 31);
       const bool want = envm ? !strcmp(envm, "msplit") : (!c->tables.single && c->tables.g == 0);
         if (eligible && want) {

@@ -77,7 +77,8 @@ __device__ __forceinline__ void ms_lds_or_bytes(uint32_t a, uint32_t v) {
   const uint32_t s = a << 3;                                   // low 5 bits: 8 * (a & 3)
   const uint32_t lo = v << (s & 31u);
   const uint32_t hi = __builtin_amdgcn_ubfe(v, (32u - s) & 31u, s & 31u);  // width 0 -> 0
-  asm volatile("ds_or_b32 %0, %1\n\tds_or_b32 %0, %2 offset:4" :: "v"(a & ~3u), "v"(lo), "v"(hi) : "memory");
+  asm volatile("ds_or_b32 %0, %1" :: "v"(a & ~3u), "v"(lo) : "memory");
+  if (hi) asm volatile("ds_or_b32 %0, %1 offset:4" :: "v"(a & ~3u), "v"(hi) : "memory");  // bytes crossed over
 }
 // ptr += byte 1 of meta (n), one SDWA add
 __device__ __forceinline__ uint32_t ms_add_n(uint32_t ptr, uint32_t meta) {
@@ -121,11 +122,11 @@ __device__ __forceinline__ void ms_shift(Win& v, uint32_t q) {
   v.d4 = __builtin_amdgcn_alignbit(v.d4, 0u, q);
 }
 
-// allowed-ends mask for R bits left: bit e-1 set for ends e <= R (all ones if R >= 32)
+// allowed-ends mask for R bits left: bit e-1 set for ends e <= R (all ones if R >= 32).
+// R is clamped to >= 1: a finished segment then allows an end at offset 1 only,
+// which no codeword has (the path requires minlen >= 2).
 __device__ __forceinline__ uint32_t ms_rmask(int R) {
-  const uint32_t r = (uint32_t)min(max(R, 0), 31);
-  const uint32_t m = (1u << r) - 1u;
-  return R >= 32 ? 0xFFFFFFFFu : m;
+  return 0xFFFFFFFFu >> (32u - (uint32_t)min(max(R, 1), 32));
 }
 
 template <int U, int TBK, int GL>
