@@ -1537,7 +1537,14 @@ __device__ __forceinline__ void copy_out_tile(uint8_t* out, const uint8_t* stg,
   uint8_t* o = out + (goff - lb);          // 16-byte aligned
   const uint32_t nz = (lb + n + 15u) >> 4;
   for (uint32_t c = tid; c < nz; c += TBK) {
-    const uint4 A = st4[c], B = st4[c + 1];
+    uint4 A, B;
+    if (abl & 64) {  // diagnostic: no LDS reads
+      A = make_uint4(c, c + 1, c + 2, c + 3);
+      B = make_uint4(c + 4, c + 5, c + 6, c + 7);
+    } else {
+      A = st4[c];
+      B = st4[c + 1];
+    }
     const uint32_t W[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
     uint4 v;
     switch (s4) {  // wave-uniform
@@ -1801,7 +1808,9 @@ void gh_tile_kernel(const TileParams p) {
     // ---- copy tile k-2 out (its prefix was published about an iteration ago) -------
     if (have2) {
       unsigned long long goff = 0;
-      if (lane == 0) {
+      if (ABLATE(32)) {  // diagnostic: no prefix wait (wrong offsets)
+        goff = (unsigned long long)tx * 16000ull;
+      } else if (lane == 0) {
         const uint32_t r2 = tx / G;
         if (!granule_ok(p, gp, 2)) {
           if (p.stats && wid == 0) atomicAdd(p.stats, 1ull);
@@ -2266,7 +2275,7 @@ struct MsKernels {
 };
 template <int GL>
 static MsKernels ms_pair() {
-  return {(const void*)gh_ms_count_kernel<U_MS, TB_MS, GL>, (const void*)gh_ms_write_kernel<U_MS, TB_MS, GL>};
+  return {(const void*)gh_ms_count_kernel<U_MS, TB_MS, GL>, (const void*)gh_ms_write_kernel<UW_MS, TBW_MS, GL>};
 }
 static MsKernels ms_kernels(uint32_t K) {
   const int g = ms_group(K);
@@ -2311,15 +2320,15 @@ static int ms_setup(gh_ctx* c) {
   c->ntiles = (uint32_t)ceil_div(c->nseg, (uint64_t)U_MS * TB_MS);
   // codewords per segment: wholly inside [start, E), E - start <= 143
   const uint32_t maxsyms = std::min<uint32_t>(143 / std::max<uint32_t>(cn.minlen, 1) + 1, 255);
-  // Staging: the most workgroups per CU (4, 3, 2) whose staging still holds one
+  // Staging: the most workgroups per CU (8 .. 1) whose staging still holds one
   // chain's worst case (TB_MS segments x maxsyms); a tile that exceeds it is staged
   // one chain at a time (gh_ms_write_kernel).
-  constexpr int NW = TB_MS / 64;
-  const size_t misc = 4 * (U_MS * NW + 2) + 8 * NW;
-  const size_t chain_worst = (size_t)TB_MS * maxsyms + 64 + 32;
-  const size_t full_worst = (size_t)U_MS * TB_MS * maxsyms + 64 + 32;
+  constexpr int NW = TBW_MS / 64;
+  const size_t misc = 4 * (UW_MS * NW + 2) + 8 * NW;
+  const size_t chain_worst = (size_t)TBW_MS * maxsyms + 64 + 32;
+  const size_t full_worst = (size_t)UW_MS * TBW_MS * maxsyms + 64 + 32;
   size_t stage = 0;
-  for (int wg = 4; wg >= 1 && stage == 0; --wg) {
+  for (int wg = 8; wg >= 1 && stage == 0; --wg) {
     const long avail = (long)(163840 / wg) - (long)lb - (long)misc;
     if (avail >= (long)chain_worst) stage = std::min<size_t>((size_t)avail & ~15ull, (full_worst + 15) & ~15ull);
   }
@@ -2332,7 +2341,7 @@ static int ms_setup(gh_ctx* c) {
   int pc_c = 0, pc_w = 0;
   const MsKernels mk = ms_kernels(K);
   GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc_c, mk.count, TB_MS, c->lds_count));
-  GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc_w, mk.write, TB_MS, c->lds));
+  GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc_w, mk.write, TBW_MS, c->lds));
   if (pc_c < 1 || pc_w < 1) return fail(GH_E_HIP, "msplit kernels do not fit on a CU");
   c->grid = (uint32_t)std::min<uint64_t>(c->ntiles, (uint64_t)pc_w * c->num_cu);
   // count ranges nest in write ranges (floor(b*n/grid) boundaries coincide for
@@ -2928,7 +2937,7 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     aw[0] = &mw;
     const MsKernels mk = ms_kernels(c->ms_k);
     GH_HIP(hipLaunchKernel(mk.count, dim3(c->grid * c->count_per), dim3(TB_MS), ac, c->lds_count, st));
-    GH_HIP(hipLaunchKernel(mk.write, dim3(c->grid), dim3(TB_MS), aw, c->lds, st));
+    GH_HIP(hipLaunchKernel(mk.write, dim3(c->grid), dim3(TBW_MS), aw, c->lds, st));
   } else if (c->tile) {
     TileParams t{};
     t.payload = c->d_payload;
