@@ -271,6 +271,12 @@ extern "C" int gh_encode_plan_make(const uint8_t* in, uint64_t n, int threads,
   });
   for (int t = 0; t < nt; ++t)
     for (int v = 0; v < 256; ++v) plan->count[v] += hist[(size_t)t * 256 + v];
+  return gh::plan_from_counts(plan, force_version);
+}
+
+// The plan from plan->n and plan->count[] (the host histogram above, or the GPU
+// encoder's, gh_encode.hip).
+int gh::plan_from_counts(gh_encode_plan* plan, int force_version) {
   // store_symbols (symbols.cpp:29-43): ascending symbol value, non-zero counts;
   // then a stable ascending sort by count (huff.cpp:115).
   uint32_t order[256];
@@ -303,7 +309,7 @@ extern "C" int gh_encode_plan_make(const uint8_t* in, uint64_t n, int threads,
   plan->g = ceil_div(bits, GH_SEGMENT_BITS);
   plan->w = ceil_div(bits, 32);
   const uint64_t lim = 1ull << 31;
-  plan->version = (n >= lim || plan->w >= lim || plan->g >= lim) ? 2 : 1;
+  plan->version = (plan->n >= lim || plan->w >= lim || plan->g >= lim) ? 2 : 1;
   if (force_version == 2) plan->version = 2;
   if (force_version == 1 && plan->version == 2)
     return fail(GH_E_ARG, "stream too large for the v1 (32-bit) header");
@@ -312,13 +318,9 @@ extern "C" int gh_encode_plan_make(const uint8_t* in, uint64_t n, int threads,
   return GH_OK;
 }
 
-extern "C" int gh_encode_write(const uint8_t* in, const gh_encode_plan* plan, int threads,
-                               void* out_v, uint64_t out_len) {
-  if (!plan || !out_v || (plan->n && !in)) return fail(GH_E_ARG, "null argument");
-  if (out_len < plan->file_bytes) return fail(GH_E_SMALL, "output buffer too small");
-  uint8_t* out = (uint8_t*)out_v;
-  const uint64_t n = plan->n, W = plan->w, G = plan->g;
-  const uint64_t GW = ceil_div(G, GH_GAPS_PER_WORD);
+// Header of the compressed image (encoder/src/huff.cpp:186-196; v2: 64-bit sizes
+// behind a magic); returns its size in bytes.
+size_t gh::encode_header(const gh_encode_plan* plan, uint8_t* out) {
   size_t off = 0;
   if (plan->version == 2) {
     wr<uint64_t>(out, GH_V2_MAGIC);
@@ -331,16 +333,27 @@ extern "C" int gh_encode_write(const uint8_t* in, const gh_encode_plan* plan, in
     out[off++] = plan->syms[i].length;
   }
   if (plan->version == 2) {
-    wr<uint64_t>(out + off, n);
-    wr<uint64_t>(out + off + 8, W);
-    wr<uint64_t>(out + off + 16, G);
+    wr<uint64_t>(out + off, plan->n);
+    wr<uint64_t>(out + off + 8, plan->w);
+    wr<uint64_t>(out + off + 16, plan->g);
     off += 24;
   } else {
-    wr<uint32_t>(out + off, (uint32_t)n);
-    wr<uint32_t>(out + off + 4, (uint32_t)W);
-    wr<uint32_t>(out + off + 8, (uint32_t)G);
+    wr<uint32_t>(out + off, (uint32_t)plan->n);
+    wr<uint32_t>(out + off + 4, (uint32_t)plan->w);
+    wr<uint32_t>(out + off + 8, (uint32_t)plan->g);
     off += 12;
   }
+  return off;
+}
+
+extern "C" int gh_encode_write(const uint8_t* in, const gh_encode_plan* plan, int threads,
+                               void* out_v, uint64_t out_len) {
+  if (!plan || !out_v || (plan->n && !in)) return fail(GH_E_ARG, "null argument");
+  if (out_len < plan->file_bytes) return fail(GH_E_SMALL, "output buffer too small");
+  uint8_t* out = (uint8_t*)out_v;
+  const uint64_t n = plan->n, W = plan->w, G = plan->g;
+  const uint64_t GW = ceil_div(G, GH_GAPS_PER_WORD);
+  size_t off = gh::encode_header(plan, out);
   std::vector<uint32_t> gaps(GW + 1, 0), words(W + 1, 0);
   const int nt = (int)std::min<uint64_t>(n_threads(threads), std::max<uint64_t>(1, n >> 20));
   // per-thread bit totals -> exclusive bit offsets

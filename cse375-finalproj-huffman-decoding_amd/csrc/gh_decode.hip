@@ -1521,66 +1521,40 @@ __device__ __forceinline__ void emit_chain(Win v, int start, bool act, uint32_t 
 
 // Copy a tile staged at staging byte STAGE_PAD + i = tile byte i to out[goff, goff+n)
 // (n already clamped at out_cap).  Output chunk c (16 bytes, aligned to the global
-// address) is staging bytes [16c + s, 16c + s + 16), s = 16 - (goff & 15): two
-// conflict-free ds_read_b128 and a funnel by the wave-uniform s.  Interior chunks
-// are one 16-byte store; the (at most two) partial edge chunks are finished byte by
-// byte by the lanes that own them.
-template <int TBK>
-__device__ __forceinline__ void copy_out_tile(uint8_t* out, const uint8_t* stg,
-                                              unsigned long long goff, uint32_t n, int tid,
-                                              uint32_t abl = 0) {
-  if (n == 0) return;
-  const uint4* st4 = (const uint4*)stg;
-  const uint32_t lb = (uint32_t)(goff & 15);
-  const uint32_t s = 16u - lb;             // 1..16, uniform
-  const uint32_t s4 = s >> 2, s1 = s & 3u;
-  uint8_t* o = out + (goff - lb);          // 16-byte aligned
-  const uint32_t nz = (lb + n + 15u) >> 4;
-  for (uint32_t c = tid; c < nz; c += TBK) {
-    uint4 A, B;
-    if (abl & 64) {  // diagnostic: no LDS reads
-      A = make_uint4(c, c + 1, c + 2, c + 3);
-      B = make_uint4(c + 4, c + 5, c + 6, c + 7);
-    } else {
-      A = st4[c];
-      B = st4[c + 1];
-    }
-    const uint32_t W[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
-    uint4 v;
-    switch (s4) {  // wave-uniform
-      case 0:
-        v = make_uint4(__builtin_amdgcn_alignbyte(W[1], W[0], s1), __builtin_amdgcn_alignbyte(W[2], W[1], s1),
-                       __builtin_amdgcn_alignbyte(W[3], W[2], s1), __builtin_amdgcn_alignbyte(W[4], W[3], s1));
-        break;
-      case 1:
-        v = make_uint4(__builtin_amdgcn_alignbyte(W[2], W[1], s1), __builtin_amdgcn_alignbyte(W[3], W[2], s1),
-                       __builtin_amdgcn_alignbyte(W[4], W[3], s1), __builtin_amdgcn_alignbyte(W[5], W[4], s1));
-        break;
-      case 2:
-        v = make_uint4(__builtin_amdgcn_alignbyte(W[3], W[2], s1), __builtin_amdgcn_alignbyte(W[4], W[3], s1),
-                       __builtin_amdgcn_alignbyte(W[5], W[4], s1), __builtin_amdgcn_alignbyte(W[6], W[5], s1));
-        break;
-      case 3:
-        v = make_uint4(__builtin_amdgcn_alignbyte(W[4], W[3], s1), __builtin_amdgcn_alignbyte(W[5], W[4], s1),
-                       __builtin_amdgcn_alignbyte(W[6], W[5], s1), __builtin_amdgcn_alignbyte(W[7], W[6], s1));
-        break;
-      default:  // s == 16
-        v = make_uint4(W[4], W[5], W[6], W[7]);
-        break;
-    }
-    // tile bytes covered by this chunk: [16c - lb, 16c - lb + 16)
-    const int r0 = (int)(16u * c) - (int)lb;
-    if (r0 >= 0 && r0 + 16 <= (int)n) {
-      if (!(abl & 16) || v.x == 0x9E3779B9u) *(uint4*)(o + 16ull * c) = v;
-    } else {  // edge chunk: bytes [k0, k1) of it belong to the tile
-      const int k0 = max(0, -r0), k1 = min(16, (int)n - r0);
-      uint8_t* oc = o + 16ull * c;
+// address) is staging bytes [16c + s, 16c + s + 16), s = 16 - (goff & 15): one
+// unaligned ds_read_b128 (gfx950 LDS runs in unaligned mode).  Interior chunks are
+// one 16-byte store each; the (at most two) partial edge chunks are finished byte by
+// byte by two lanes.  stg: absolute LDS byte address of the staging buffer.
+__device__ __forceinline__ uint4 lds_u128(uint32_t byte_addr) {
+  uint4 v;
+  asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(byte_addr) : "memory");
+  return v;
+}
+__device__ __forceinline__ void store_edge(uint8_t* oc, uint4 v, int k0, int k1) {
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const uint32_t wv = k < 4 ? v.x : k < 8 ? v.y : k < 12 ? v.z : v.w;
-        if (k >= k0 && k < k1) oc[k] = (uint8_t)(wv >> (8 * (k & 3)));
-      }
-    }
+  for (int k = 0; k < 16; ++k) {
+    const uint32_t wv = k < 4 ? v.x : k < 8 ? v.y : k < 12 ? v.z : v.w;
+    if (k >= k0 && k < k1) oc[k] = (uint8_t)(wv >> (8 * (k & 3)));
+  }
+}
+template <int TBK>
+__device__ __forceinline__ void copy_out_tile(uint8_t* out, uint32_t stg, unsigned long long goff, uint32_t n,
+                                              int tid, uint32_t abl = 0) {
+  if (n == 0) return;
+  const uint32_t lb = (uint32_t)(goff & 15);
+  uint8_t* o = out + (goff - lb);          // 16-byte aligned
+  const uint32_t src = stg + 16u - lb;     // staging address of output chunk 0
+  const uint32_t cf = lb ? 1u : 0u;        // interior chunks [cf, ce)
+  const uint32_t ce = (lb + n) >> 4;
+  for (uint32_t c = cf + (uint32_t)tid; c < ce; c += TBK) {
+    const uint4 v = (abl & 64) ? make_uint4(c, c + 1, c + 2, c + 3) : lds_u128(src + 16u * c);
+    if (!(abl & 16) || v.x == 0x9E3779B9u) *(uint4*)(o + 16ull * c) = v;
+  }
+  const uint32_t tail = (lb + n) & 15u;
+  if (tid == 0 && lb) {  // first chunk: tile bytes [0, 16 - lb), or all n if the tile ends in it
+    store_edge(o, lds_u128(src), (int)lb, (int)min(16u, lb + n));
+  } else if (tid == TBK - 1 && tail && (ce > 0 || !lb)) {  // last chunk ce: bytes [0, tail)
+    store_edge(o + 16ull * ce, lds_u128(src + 16u * ce), 0, (int)tail);
   }
 }
 
@@ -1828,8 +1802,8 @@ void gh_tile_kernel(const TileParams p) {
       STAMP(6);
       const uint32_t n2 =
           goff >= p.out_cap ? 0u : (uint32_t)min<unsigned long long>(LAG3 ? tot3 : tot2, p.out_cap - goff);
-      if (!ABLATE(2)) copy_out_tile<TB>(p.out, s_stage + (LAG3 ? buf ^ 1u : buf) * p.stage_bytes, goff, n2, tid,
-                                      p.ablate);
+      if (!ABLATE(2)) copy_out_tile<TB>(p.out, p.lut_bytes + (LAG3 ? buf ^ 1u : buf) * p.stage_bytes, goff, n2, tid,
+                                      (uint32_t)ABLATE(0xFFFFFFFFu));
     }
     STAMP(1);
 #if GH_PREFETCH_LATE

@@ -1,0 +1,458 @@
+// GPU encoder of the compressed.huff format: the reference's
+// encoder.cu pipeline (histogram :118-140, cuencoder :142-355, cu_get_gaparray
+// :358-379) re-designed for gfx950.  Byte-identical to the host encoder
+// (gh_core.cpp gh_encode_write), which restates the reference's packing: codewords
+// MSB-first inside u32 words; for every codeword crossing a 128-bit boundary, the
+// nibble (end bit mod 16) at the index of the segment it starts in, 8 nibbles per
+// u32, LSB-first.
+//
+// Kernels (input resident in HBM, 4 KiB chunks of 256 threads x 16 bytes):
+//   gh_enc_hist_kernel   byte histogram; LDS counters replicated 32x (lane & 31), so
+//                        one instruction's lanes collide at most 2-way even on the
+//                        skewed r=0.9 data; 256 u64 atomics per workgroup.
+//   (host)               package-merge + canonical codes (gh::plan_from_counts).
+//   gh_enc_bits_kernel   code bits per chunk (u32).
+//   gh_enc_scan_kernel   exclusive scan of the chunk bits in blocks of 8192 chunks,
+//   gh_enc_blkscan_kernel  then of the block totals (u64).
+//   gh_enc_write_kernel  one chunk per workgroup: block scan of the lanes' bits,
+//                        codewords OR-ed
+//                        into a zeroed LDS image of the chunk's words (positions in
+//                        32 bits relative to the chunk's gap-word-aligned base),
+//                        then written with coalesced stores.  No payload atomics: a
+//                        chunk owns the words whose first bit it holds, and its last
+//                        lane encodes the next chunk's first symbols (< 32 bits) to
+//                        complete its last word.  Gap nibbles likewise in LDS; the two
+//                        edge gap words of a chunk (shared with its neighbours) are
+//                        atomicOr-ed into the zeroed gap array, the rest stored.
+// Traffic: N (histogram, plan step) + 2N + C + gaps (encode) bytes.  A single pass
+// with a decoupled look-back (one 4 KiB chunk per workgroup) measured 2.85 ms on
+// cfg4, slower than these three kernels: its workgroups waited on their nearest
+// predecessors' aggregates.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <vector>
+
+#include "gaphuff.h"
+#include "gh_internal.hpp"
+
+namespace gh {
+
+constexpr int ETB = 256;                 // threads per workgroup
+constexpr int EBPT = 16;                 // input bytes per thread
+constexpr int ECHUNK = ETB * EBPT;       // input bytes per chunk
+constexpr int EREP = 32;                 // histogram replicas
+// LDS image of a chunk from its gap-word-aligned base: up to 1023 bits before it,
+// 16 bits per byte, the last word's completion (< 32 + 16 bits)
+constexpr int EWORDS = (1024 + ECHUNK * GH_MAX_CODE_LEN + 64) / 32 + 2;
+constexpr int EGAPW = (1024 + ECHUNK * GH_MAX_CODE_LEN) / 1024 + 2;
+
+__device__ __forceinline__ uint32_t enc_byte(const uint4& v, int k) {
+  const uint32_t w = k < 4 ? v.x : k < 8 ? v.y : k < 12 ? v.z : v.w;
+  return (w >> (8 * (k & 3))) & 0xFFu;
+}
+
+// 16 input bytes of thread t of chunk c (bytes past n read as "absent": 0x100).
+__device__ __forceinline__ void enc_load(const uint8_t* in, uint64_t n, uint64_t base, uint32_t (&b)[EBPT]) {
+  if (base + EBPT <= n) {
+    const uint4 v = *(const uint4*)(in + base);
+#pragma unroll
+    for (int k = 0; k < EBPT; ++k) b[k] = enc_byte(v, k);
+  } else {
+#pragma unroll
+    for (int k = 0; k < EBPT; ++k) b[k] = base + k < n ? (uint32_t)in[base + k] : 0x100u;
+  }
+}
+
+__global__ __launch_bounds__(ETB) void gh_enc_hist_kernel(const uint8_t* in, uint64_t n,
+                                                          unsigned long long* count) {
+  __shared__ uint32_t h[256 * EREP];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 256 * EREP; i += ETB) h[i] = 0;
+  __syncthreads();
+  const uint32_t rep = (uint32_t)tid & (EREP - 1);
+  const uint64_t nchunks = (n + ECHUNK - 1) / ECHUNK;
+  for (uint64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    uint32_t b[EBPT];
+    enc_load(in, n, c * ECHUNK + (uint64_t)tid * EBPT, b);
+#pragma unroll
+    for (int k = 0; k < EBPT; ++k)
+      if (b[k] < 256u) atomicAdd(&h[b[k] * EREP + rep], 1u);
+  }
+  __syncthreads();
+  for (int v = tid; v < 256; v += ETB) {
+    unsigned long long s = 0;
+#pragma unroll
+    for (int r = 0; r < EREP; ++r) s += h[v * EREP + ((r + v) & (EREP - 1))];
+    if (s) atomicAdd(&count[v], s);
+  }
+}
+
+// Workgroup exclusive scan of one u32 per thread; returns the exclusive prefix and
+// sets total.  s_red: NWAVE u32 of LDS.
+__device__ __forceinline__ uint32_t enc_block_scan(uint32_t x, uint32_t* s_red, uint32_t& total) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  uint32_t incl = x;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += y;
+  }
+  if (lane == 63) s_red[wid] = incl;
+  __syncthreads();
+  uint32_t before = 0;
+  total = 0;
+#pragma unroll
+  for (int q = 0; q < ETB / 64; ++q) {
+    const uint32_t v = s_red[q];
+    before += q < wid ? v : 0u;
+    total += v;
+  }
+  return before + incl - x;
+}
+
+__global__ __launch_bounds__(ETB) void gh_enc_bits_kernel(const uint8_t* in, uint64_t n, const uint32_t* lut,
+                                                          uint32_t* chunk_bits) {
+  __shared__ uint32_t s_len[257];
+  __shared__ uint32_t s_red[ETB / 64];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 256; i += ETB) s_len[i] = lut[i] & 0xFFu;
+  if (tid == 0) s_len[256] = 0;
+  uint32_t b[EBPT];
+  enc_load(in, n, (uint64_t)blockIdx.x * ECHUNK + (uint64_t)tid * EBPT, b);
+  __syncthreads();
+  uint32_t bits = 0;
+#pragma unroll
+  for (int k = 0; k < EBPT; ++k) bits += s_len[b[k]];
+  uint32_t total;
+  (void)enc_block_scan(bits, s_red, total);
+  if (tid == 0) chunk_bits[blockIdx.x] = total;
+}
+
+// Chunk offsets in two levels.  gh_enc_scan_kernel: workgroup k scans chunks
+// [8192k, 8192k + 8192) (8 consecutive per thread): local exclusive offsets and the
+// block total.  gh_enc_blkscan_kernel (one workgroup): exclusive scan of the block
+// totals.  The write kernel adds the two.
+constexpr int SCAN_TB = 1024, SCAN_PT = 8, SCAN_BLK = SCAN_TB * SCAN_PT;
+__global__ __launch_bounds__(SCAN_TB) void gh_enc_scan_kernel(const uint32_t* chunk_bits, uint32_t nchunks,
+                                                              uint32_t* chunk_loc, unsigned long long* blk_tot) {
+  __shared__ uint32_t s_w[SCAN_TB / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const uint32_t i0 = blockIdx.x * (uint32_t)SCAN_BLK + (uint32_t)tid * SCAN_PT;
+  uint32_t v[SCAN_PT], t = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_PT; ++k) v[k] = i0 + k < nchunks ? chunk_bits[i0 + k] : 0u;
+#pragma unroll
+  for (int k = 0; k < SCAN_PT; ++k) {
+    const uint32_t x = v[k];
+    v[k] = t;  // exclusive within the thread
+    t += x;
+  }
+  uint32_t incl = t;  // a block holds <= 2^29 bits (8192 chunks x 65536)
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += y;
+  }
+  if (lane == 63) s_w[wid] = incl;
+  __syncthreads();
+  uint32_t before = 0, tot = 0;
+#pragma unroll
+  for (int q = 0; q < SCAN_TB / 64; ++q) {
+    const uint32_t x = s_w[q];
+    before += q < wid ? x : 0u;
+    tot += x;
+  }
+  const uint32_t b0 = before + incl - t;
+#pragma unroll
+  for (int k = 0; k < SCAN_PT; ++k)
+    if (i0 + k < nchunks) chunk_loc[i0 + k] = b0 + v[k];
+  if (tid == 0) blk_tot[blockIdx.x] = tot;
+}
+__global__ __launch_bounds__(SCAN_TB) void gh_enc_blkscan_kernel(unsigned long long* blk, uint32_t nblk) {
+  __shared__ unsigned long long s[SCAN_TB];
+  const int tid = threadIdx.x;
+  unsigned long long carry = 0;
+  for (uint32_t base = 0; base < nblk; base += SCAN_TB) {
+    const uint32_t i = base + (uint32_t)tid;
+    const unsigned long long x = i < nblk ? blk[i] : 0ull;
+    s[tid] = x;
+    __syncthreads();
+    for (int d = 1; d < SCAN_TB; d <<= 1) {
+      const unsigned long long y = tid >= d ? s[tid - d] : 0ull;
+      __syncthreads();
+      s[tid] += y;
+      __syncthreads();
+    }
+    if (i < nblk) blk[i] = carry + s[tid] - x;
+    carry += s[SCAN_TB - 1];
+    __syncthreads();
+  }
+}
+
+struct EncParams {
+  const uint8_t* in;
+  const uint32_t* lut;                 // 256 x {code << 8 | len}
+  const uint32_t* chunk_loc;           // bit offset of each chunk within its scan block
+  const unsigned long long* blk_off;   // bit offset of each scan block
+  uint32_t* words;                     // W payload words
+  uint32_t* gaps;                      // GW gap words, zeroed
+  uint64_t n;
+};
+
+__global__ __launch_bounds__(ETB) void gh_enc_write_kernel(const EncParams p) {
+  __shared__ uint32_t s_lut[257];
+  __shared__ uint32_t s_w[EWORDS];
+  __shared__ uint32_t s_g[EGAPW];
+  __shared__ uint32_t s_red[ETB / 64];
+  const int tid = threadIdx.x;
+  const uint32_t c = blockIdx.x;
+  for (int i = tid; i < 256; i += ETB) s_lut[i] = p.lut[i];
+  if (tid == 0) s_lut[256] = 0;
+  for (int i = tid; i < EWORDS; i += ETB) s_w[i] = 0;
+  for (int i = tid; i < EGAPW; i += ETB) s_g[i] = 0;
+  const unsigned long long off0 = p.blk_off[c / SCAN_BLK] + p.chunk_loc[c];
+  uint32_t b[EBPT];
+  enc_load(p.in, p.n, (uint64_t)c * ECHUNK + (uint64_t)tid * EBPT, b);
+  __syncthreads();
+  uint32_t bits = 0;
+#pragma unroll
+  for (int k = 0; k < EBPT; ++k) bits += s_lut[b[k]] & 0xFFu;
+  uint32_t cbits;
+  const uint32_t excl = enc_block_scan(bits, s_red, cbits);
+  // positions relative to B = off0 rounded down to a gap word (1024 bits): 128-bit
+  // boundaries, payload words and gap words keep their alignment, in 32 bits
+  const unsigned long long B = off0 & ~1023ull;
+  const uint32_t qs = (uint32_t)(off0 - B);  // chunk start
+  const uint32_t qend = qs + cbits;          // chunk end (the next chunk's first bit)
+  uint32_t q = qs + excl;
+  uint32_t lw = q >> 5;                      // LDS word being filled
+  int nb = (int)(q & 31);                    // pending bits in acc (the first q & 31 are zeros)
+  uint64_t acc = 0;
+  auto put = [&](uint32_t e) {
+    const uint32_t l = e & 0xFFu;
+    const uint32_t qe = q + l;
+    if ((qe ^ q) >= 128u) {  // crosses a 128-bit boundary
+      const uint32_t gv = qe & 15u;                   // nibble of segment q >> 7
+      if (gv && q < qend) atomicOr(&s_g[q >> 10], gv << (4 * ((q >> 7) & 7u)));
+    }
+    acc = (acc << l) | (e >> 8);
+    nb += (int)l;
+    if (nb >= 32) {
+      nb -= 32;
+      atomicOr(&s_w[lw], (uint32_t)(acc >> nb));
+      ++lw;
+    }
+    q = qe;
+  };
+#pragma unroll
+  for (int k = 0; k < EBPT; ++k) put(s_lut[b[k]]);
+  if (tid == ETB - 1) {
+    // complete the chunk's last word with the next chunk's first symbols (their gap
+    // nibbles belong to that chunk: q >= qend skips them)
+    const uint32_t wend = (qend + 31u) & ~31u;
+    for (uint64_t i = (uint64_t)(c + 1) * ECHUNK; q < wend && i < p.n; ++i) put(s_lut[p.in[i]]);
+  }
+  if (nb > 0) atomicOr(&s_w[lw], (uint32_t)(acc << (32 - nb)));
+  __syncthreads();
+  // payload words whose first bit lies in [off0, off0 + cbits): local [w0, w1)
+  const uint32_t w0 = (qs + 31u) >> 5, w1 = (qend + 31u) >> 5;
+  uint32_t* wout = p.words + (B >> 5);
+  for (uint32_t i = w0 + tid; i < w1; i += ETB) wout[i] = s_w[i];
+  // gap words of this chunk's segments: local [0, g1]; the first and the last may
+  // hold nibbles of the neighbouring chunks
+  if (cbits) {
+    const uint32_t g1 = (qend - 1u) >> 10;
+    uint32_t* gout = p.gaps + (B >> 10);
+    for (uint32_t i = tid; i <= g1; i += ETB) {
+      const uint32_t v = s_g[i];
+      if (i == 0 || i == g1) {
+        if (v) atomicOr(&gout[i], v);
+      } else {
+        gout[i] = v;
+      }
+    }
+  }
+}
+
+}  // namespace gh
+
+using namespace gh;
+
+#define GH_EHIP(expr)                                                             \
+  do {                                                                            \
+    hipError_t e_ = (expr);                                                       \
+    if (e_ != hipSuccess)                                                         \
+      return fail(GH_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));   \
+  } while (0)
+
+struct gh_ectx {
+  int device = 0;
+  int num_cu = 0;
+  hipStream_t stream = nullptr;
+  uint8_t* d_in = nullptr;
+  uint64_t n = 0, in_cap = 0;
+  unsigned long long* d_count = nullptr;   // 256
+  uint32_t* d_lut = nullptr;               // 256
+  uint32_t* d_chunk_bits = nullptr;
+  unsigned long long* d_chunk_off = nullptr;
+  uint64_t chunk_cap = 0;
+  uint32_t* d_words = nullptr;
+  uint32_t* d_gaps = nullptr;
+  uint64_t words_cap = 0, gaps_cap = 0;
+  gh_encode_plan plan{};
+  bool planned = false, encoded = false;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+extern "C" int gh_ectx_create(int device, gh_ectx** out) {
+  if (!out) return fail(GH_E_ARG, "null ctx pointer");
+  *out = nullptr;
+  int nd = 0;
+  if (hipGetDeviceCount(&nd) != hipSuccess || nd == 0)
+    return fail(GH_E_NODEV, "no HIP device visible (the GPU encoder has no CPU fallback)");
+  if (device < 0 || device >= nd) return fail(GH_E_ARG, "device ordinal out of range");
+  hipDeviceProp_t prop;
+  GH_EHIP(hipGetDeviceProperties(&prop, device));
+  if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
+    return fail(GH_E_NODEV, std::string("device is ") + prop.gcnArchName + ", need gfx950");
+  GH_EHIP(hipSetDevice(device));
+  gh_ectx* e = new gh_ectx();
+  e->device = device;
+  e->num_cu = prop.multiProcessorCount;
+  GH_EHIP(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+  GH_EHIP(hipMalloc(&e->d_count, 256 * 8));
+  GH_EHIP(hipMalloc(&e->d_lut, 256 * 4));
+  GH_EHIP(hipEventCreate(&e->ev0));
+  GH_EHIP(hipEventCreate(&e->ev1));
+  *out = e;
+  return GH_OK;
+}
+
+extern "C" int gh_ectx_destroy(gh_ectx* e) {
+  if (!e) return GH_OK;
+  (void)hipSetDevice(e->device);
+  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  for (void* p : {(void*)e->d_in, (void*)e->d_count, (void*)e->d_lut, (void*)e->d_chunk_bits,
+                  (void*)e->d_chunk_off, (void*)e->d_words, (void*)e->d_gaps})
+    (void)hipFree(p);
+  if (e->ev0) (void)hipEventDestroy(e->ev0);
+  if (e->ev1) (void)hipEventDestroy(e->ev1);
+  if (e->stream) (void)hipStreamDestroy(e->stream);
+  delete e;
+  return GH_OK;
+}
+
+extern "C" int gh_ectx_load(gh_ectx* e, const uint8_t* in, uint64_t n) {
+  if (!e || (n && !in)) return fail(GH_E_ARG, "null argument");
+  GH_EHIP(hipSetDevice(e->device));
+  if (n + 16 > e->in_cap) {
+    (void)hipFree(e->d_in);
+    e->d_in = nullptr;
+    e->in_cap = 0;
+    GH_EHIP(hipMalloc(&e->d_in, n + 16));
+    e->in_cap = n + 16;
+  }
+  if (n) GH_EHIP(hipMemcpyAsync(e->d_in, in, n, hipMemcpyHostToDevice, e->stream));
+  GH_EHIP(hipStreamSynchronize(e->stream));
+  e->n = n;
+  e->planned = e->encoded = false;
+  return GH_OK;
+}
+
+extern "C" int gh_ectx_plan(gh_ectx* e, int force_version, gh_encode_plan* plan) {
+  if (!e) return fail(GH_E_ARG, "null ctx");
+  GH_EHIP(hipSetDevice(e->device));
+  GH_EHIP(hipMemsetAsync(e->d_count, 0, 256 * 8, e->stream));
+  const uint64_t nchunks = ceil_div(e->n, ECHUNK);
+  if (nchunks) {
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(nchunks, 4ull * e->num_cu);
+    hipLaunchKernelGGL(gh_enc_hist_kernel, dim3(grid), dim3(ETB), 0, e->stream, e->d_in, e->n, e->d_count);
+    GH_EHIP(hipGetLastError());
+  }
+  gh_encode_plan& pl = e->plan;
+  std::memset(&pl, 0, sizeof(pl));
+  pl.n = e->n;
+  GH_EHIP(hipMemcpyAsync(pl.count, e->d_count, 256 * 8, hipMemcpyDeviceToHost, e->stream));
+  GH_EHIP(hipStreamSynchronize(e->stream));
+  const int rc = plan_from_counts(&pl, force_version);
+  if (rc) return rc;
+  e->planned = true;
+  e->encoded = false;
+  if (plan) *plan = pl;
+  return GH_OK;
+}
+
+extern "C" int gh_ectx_encode(gh_ectx* e, float* kernel_ms) {
+  if (!e) return fail(GH_E_ARG, "null ctx");
+  if (!e->planned) return fail(GH_E_STATE, "gh_ectx_encode before gh_ectx_plan");
+  GH_EHIP(hipSetDevice(e->device));
+  const gh_encode_plan& pl = e->plan;
+  for (int v = 0; v < 256; ++v)
+    if (pl.len[v] > GH_MAX_CODE_LEN) return fail(GH_E_TABLE, "code longer than 16 bits");
+  uint32_t lut[256];
+  for (int v = 0; v < 256; ++v) lut[v] = (pl.code[v] << 8) | pl.len[v];
+  const uint64_t nchunks = ceil_div(e->n, ECHUNK);
+  const uint64_t GW = ceil_div(pl.g, GH_GAPS_PER_WORD);
+  if (nchunks + 1 > e->chunk_cap) {
+    (void)hipFree(e->d_chunk_bits);
+    (void)hipFree(e->d_chunk_off);
+    e->d_chunk_bits = nullptr;
+    e->d_chunk_off = nullptr;
+    e->chunk_cap = 0;
+    GH_EHIP(hipMalloc(&e->d_chunk_bits, 4 * (nchunks + 1)));
+    GH_EHIP(hipMalloc(&e->d_chunk_off, 4 * (nchunks + 1) + 8 * (nchunks / SCAN_BLK + 2) + 64));
+    e->chunk_cap = nchunks + 1;
+  }
+  if (pl.w + 4 > e->words_cap) {
+    (void)hipFree(e->d_words);
+    e->d_words = nullptr;
+    e->words_cap = 0;
+    GH_EHIP(hipMalloc(&e->d_words, 4 * (pl.w + 4)));
+    e->words_cap = pl.w + 4;
+  }
+  if (GW + 4 > e->gaps_cap) {
+    (void)hipFree(e->d_gaps);
+    e->d_gaps = nullptr;
+    e->gaps_cap = 0;
+    GH_EHIP(hipMalloc(&e->d_gaps, 4 * (GW + 4)));
+    e->gaps_cap = GW + 4;
+  }
+  if (nchunks >= (1ull << 32)) return fail(GH_E_ARG, "input too large for the GPU encoder");
+  GH_EHIP(hipMemcpyAsync(e->d_lut, lut, sizeof(lut), hipMemcpyHostToDevice, e->stream));
+  GH_EHIP(hipEventRecord(e->ev0, e->stream));
+  GH_EHIP(hipMemsetAsync(e->d_gaps, 0, 4 * (GW + 4), e->stream));
+  if (nchunks) {
+    hipLaunchKernelGGL(gh_enc_bits_kernel, dim3((uint32_t)nchunks), dim3(ETB), 0, e->stream, e->d_in, e->n,
+                       e->d_lut, e->d_chunk_bits);
+    const uint32_t nblk = (uint32_t)ceil_div(nchunks, SCAN_BLK);
+    uint32_t* loc = (uint32_t*)e->d_chunk_off;
+    unsigned long long* blk = e->d_chunk_off + (nchunks + 2) / 2 + 1;  // after the local offsets
+    hipLaunchKernelGGL(gh_enc_scan_kernel, dim3(nblk), dim3(SCAN_TB), 0, e->stream, e->d_chunk_bits,
+                       (uint32_t)nchunks, loc, blk);
+    hipLaunchKernelGGL(gh_enc_blkscan_kernel, dim3(1), dim3(SCAN_TB), 0, e->stream, blk, nblk);
+    EncParams p{e->d_in, e->d_lut, loc, blk, e->d_words, e->d_gaps, e->n};
+    hipLaunchKernelGGL(gh_enc_write_kernel, dim3((uint32_t)nchunks), dim3(ETB), 0, e->stream, p);
+    GH_EHIP(hipGetLastError());
+  }
+  GH_EHIP(hipEventRecord(e->ev1, e->stream));
+  GH_EHIP(hipStreamSynchronize(e->stream));
+  if (kernel_ms) GH_EHIP(hipEventElapsedTime(kernel_ms, e->ev0, e->ev1));
+  e->encoded = true;
+  return GH_OK;
+}
+
+extern "C" int gh_ectx_download(gh_ectx* e, void* out, uint64_t out_len) {
+  if (!e || !out) return fail(GH_E_ARG, "null argument");
+  if (!e->encoded) return fail(GH_E_STATE, "gh_ectx_download before gh_ectx_encode");
+  const gh_encode_plan& pl = e->plan;
+  if (out_len < pl.file_bytes) return fail(GH_E_SMALL, "output buffer too small");
+  GH_EHIP(hipSetDevice(e->device));
+  uint8_t* o = (uint8_t*)out;
+  const size_t hdr = encode_header(&pl, o);
+  const uint64_t GW = ceil_div(pl.g, GH_GAPS_PER_WORD);
+  if (GW) GH_EHIP(hipMemcpyAsync(o + hdr, e->d_gaps, 4 * GW, hipMemcpyDeviceToHost, e->stream));
+  if (pl.w) GH_EHIP(hipMemcpyAsync(o + hdr + 4 * GW, e->d_words, 4 * pl.w, hipMemcpyDeviceToHost, e->stream));
+  GH_EHIP(hipStreamSynchronize(e->stream));
+  return GH_OK;
+}

@@ -48,4 +48,10 @@ inline uint32_t canon_decode16(const Canon& c, uint32_t w16, uint32_t* index) {
 
 inline uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 
+// Encoder plan from plan->n and plan->count[] (symbol order, package-merge lengths,
+// canonical codes, sizes, header version); shared by the host and GPU encoders.
+int plan_from_counts(gh_encode_plan* plan, int force_version);
+// Writes the image header; returns its size.  out must hold file_bytes - payload.
+size_t encode_header(const gh_encode_plan* plan, uint8_t* out);
+
 }  // namespace gh

@@ -45,6 +45,8 @@ EXPORTED = (
     "gh_ctx_load_device", "gh_ctx_decode", "gh_ctx_report", "gh_ctx_download",
     "gh_ctx_output", "gh_ctx_copy_output", "gh_ctx_reset_timing", "gh_decode", "gh_plan_shards",
     "gh_device_count", "gh_version", "gh_last_error",
+    "gh_ectx_create", "gh_ectx_destroy", "gh_ectx_load", "gh_ectx_plan", "gh_ectx_encode",
+    "gh_ectx_download",
 )
 
 
@@ -126,6 +128,12 @@ def lib() -> ctypes.CDLL:
                            ctypes.POINTER(gh_report)], I),
             "gh_plan_shards": ([U64, U32, P], I),
             "gh_device_count": ([], I),
+            "gh_ectx_create": ([I, ctypes.POINTER(P)], I),
+            "gh_ectx_destroy": ([P], I),
+            "gh_ectx_load": ([P, P, U64], I),
+            "gh_ectx_plan": ([P, I, ctypes.POINTER(gh_encode_plan)], I),
+            "gh_ectx_encode": ([P, ctypes.POINTER(ctypes.c_float)], I),
+            "gh_ectx_download": ([P, P, U64], I),
             "gh_version": ([], ctypes.c_char_p),
             "gh_last_error": ([], ctypes.c_char_p),
         }
@@ -204,6 +212,68 @@ def encode(data, threads: int = 0, force_version: int = 0) -> np.ndarray:
     out = np.empty(plan.file_bytes, dtype=np.uint8)
     _check(lib().gh_encode_write(_ptr(d), ctypes.byref(plan), threads, _ptr(out), out.size))
     return out
+
+
+class Encoder:
+    """One gh_ectx: the GPU encoder on one gfx950 device.
+
+    Mirrors the reference encoder CLI's steps (encoder/src/huff.cpp:30-220): load the
+    input, plan (histogram on the GPU, package-merge on the host), encode, download
+    the compressed.huff image -- byte-identical to ``encode()``."""
+
+    def __init__(self, device: int = 0):
+        self._h = ctypes.c_void_p()
+        _check(lib().gh_ectx_create(device, ctypes.byref(self._h)))
+        self.plan: Optional[gh_encode_plan] = None
+
+    def close(self) -> None:
+        if self._h:
+            lib().gh_ectx_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def load(self, data) -> None:
+        d = _u8(data)
+        _check(lib().gh_ectx_load(self._h, _ptr(d), d.size))
+
+    def make_plan(self, force_version: int = 0) -> gh_encode_plan:
+        p = gh_encode_plan()
+        _check(lib().gh_ectx_plan(self._h, force_version, ctypes.byref(p)))
+        self.plan = p
+        return p
+
+    def encode(self) -> float:
+        """Encode on the device; returns the kernels' event time in ms."""
+        ms = ctypes.c_float()
+        _check(lib().gh_ectx_encode(self._h, ctypes.byref(ms)))
+        return float(ms.value)
+
+    def download(self) -> np.ndarray:
+        if self.plan is None:
+            raise GapHuffError(-8, "download before make_plan/encode")
+        out = np.empty(self.plan.file_bytes, dtype=np.uint8)
+        _check(lib().gh_ectx_download(self._h, _ptr(out), out.size))
+        return out
+
+
+def encode_gpu(data, device: int = 0, force_version: int = 0) -> np.ndarray:
+    """Compress bytes on the GPU into a compressed.huff image (== ``encode(data)``)."""
+    with Encoder(device) as e:
+        e.load(data)
+        e.make_plan(force_version)
+        e.encode()
+        return e.download()
 
 
 def package_merge(sorted_counts: Sequence[int]) -> list:

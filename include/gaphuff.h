@@ -117,6 +117,25 @@ int gh_package_merge(const uint64_t* sorted_counts, uint32_t nsyms, uint8_t* len
 int gh_generate(uint64_t seed, double redundancy, uint64_t offset, uint64_t n,
                 uint8_t* out, int threads);
 
+/* ---- GPU encoder ------------------------------------ */
+/* Replaces the reference's GPU encoder: histogram (encoder/src/encoder.cu:118-140),
+ * cuencoder (:142-355) and cu_get_gaparray (:358-379) behind encoder/src/huff.cpp:
+ * 30-220.  The image is byte-identical to gh_encode_write's.  The code lengths are
+ * built on the host (package-merge) from the GPU histogram.  An encoder context is
+ * bound to one gfx950 device; no CPU fallback. */
+typedef struct gh_ectx gh_ectx;
+int gh_ectx_create(int device, gh_ectx** out);
+int gh_ectx_destroy(gh_ectx* ctx);
+/* Copy n input bytes to the device (kept resident across plan/encode calls). */
+int gh_ectx_load(gh_ectx* ctx, const uint8_t* in, uint64_t n);
+/* GPU histogram + host package-merge; fills *plan (may be NULL). */
+int gh_ectx_plan(gh_ectx* ctx, int force_version, gh_encode_plan* plan);
+/* Encode the loaded input on the device; kernel_ms (may be NULL): event time of the
+ * encode kernels, input already resident. */
+int gh_ectx_encode(gh_ectx* ctx, float* kernel_ms);
+/* Header + gap words + payload words into out (plan->file_bytes bytes). */
+int gh_ectx_download(gh_ectx* ctx, void* out, uint64_t out_len);
+
 /* ---- GPU decoder -------------------------------------------------------------- */
 typedef struct gh_ctx gh_ctx;
 

@@ -39,3 +39,13 @@ def test_no_gpu_fails_loudly(gh):
     img = gh.encode(gh.generate(1, 0.5, 1000))
     with pytest.raises(gh.GapHuffError):
         gh.decode(img)
+
+
+def test_no_gpu_encoder_fails_loudly(gh):
+    if gh.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(gh.GapHuffError) as e:
+        gh.Encoder(0)
+    assert e.value.code == -5
+    with pytest.raises(gh.GapHuffError):
+        gh.encode_gpu(gh.generate(1, 0.5, 1000))
