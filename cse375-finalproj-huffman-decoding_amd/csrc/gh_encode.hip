@@ -111,22 +111,36 @@ __device__ __forceinline__ uint32_t enc_block_scan(uint32_t x, uint32_t* s_red, 
   return before + incl - x;
 }
 
-__global__ __launch_bounds__(ETB) void gh_enc_bits_kernel(const uint8_t* in, uint64_t n, const uint32_t* lut,
-                                                          uint32_t* chunk_bits) {
+// Persistent: workgroup b takes chunks b, b + G, ...; the next chunk's bytes are
+// loaded before the current one's reduction.
+__global__ __launch_bounds__(ETB) void gh_enc_bits_kernel(const uint8_t* in, uint64_t n, uint32_t nchunks,
+                                                          const uint32_t* lut, uint32_t* chunk_bits) {
   __shared__ uint32_t s_len[257];
-  __shared__ uint32_t s_red[ETB / 64];
-  const int tid = threadIdx.x;
+  __shared__ uint32_t s_red[2][ETB / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   for (int i = tid; i < 256; i += ETB) s_len[i] = lut[i] & 0xFFu;
   if (tid == 0) s_len[256] = 0;
   uint32_t b[EBPT];
-  enc_load(in, n, (uint64_t)blockIdx.x * ECHUNK + (uint64_t)tid * EBPT, b);
+  uint32_t c = blockIdx.x;
+  if (c < nchunks) enc_load(in, n, (uint64_t)c * ECHUNK + (uint64_t)tid * EBPT, b);
   __syncthreads();
-  uint32_t bits = 0;
+  for (uint32_t it = 0; c < nchunks; c += gridDim.x, ++it) {
+    uint32_t bits = 0;
 #pragma unroll
-  for (int k = 0; k < EBPT; ++k) bits += s_len[b[k]];
-  uint32_t total;
-  (void)enc_block_scan(bits, s_red, total);
-  if (tid == 0) chunk_bits[blockIdx.x] = total;
+    for (int k = 0; k < EBPT; ++k) bits += s_len[b[k]];
+    const uint32_t cn = c + gridDim.x;
+    if (cn < nchunks) enc_load(in, n, (uint64_t)cn * ECHUNK + (uint64_t)tid * EBPT, b);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) bits += __shfl_xor(bits, d, 64);
+    if (lane == 0) s_red[it & 1][wid] = bits;
+    __syncthreads();  // (double-buffered partial sums: one barrier per chunk)
+    if (tid == 0) {
+      uint32_t t = 0;
+#pragma unroll
+      for (int q = 0; q < ETB / 64; ++q) t += s_red[it & 1][q];
+      chunk_bits[c] = t;
+    }
+  }
 }
 
 // Chunk offsets in two levels.  gh_enc_scan_kernel: workgroup k scans chunks
@@ -198,78 +212,139 @@ struct EncParams {
   uint32_t* words;                     // W payload words
   uint32_t* gaps;                      // GW gap words, zeroed
   uint64_t n;
+  uint32_t nchunks;
 };
 
+// Persistent: workgroup b encodes chunks b, b + G, ...  The next chunk's bytes and
+// offset (and the 32 bytes after it, for its last word) are loaded while the current
+// chunk is encoded; the LDS image is re-zeroed as it is written out.
 __global__ __launch_bounds__(ETB) void gh_enc_write_kernel(const EncParams p) {
   __shared__ uint32_t s_lut[257];
   __shared__ uint32_t s_w[EWORDS];
   __shared__ uint32_t s_g[EGAPW];
-  __shared__ uint32_t s_red[ETB / 64];
-  const int tid = threadIdx.x;
-  const uint32_t c = blockIdx.x;
-  for (int i = tid; i < 256; i += ETB) s_lut[i] = p.lut[i];
+  __shared__ uint32_t s_red[2][ETB / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const uint32_t lutv = p.lut[tid & 255];
+  uint32_t c = blockIdx.x;
+  const uint32_t G = gridDim.x;
+  // chunk c's inputs: its 16 bytes per lane, its offset, and (last lane) the next 32 bytes
+  uint4 v = make_uint4(0, 0, 0, 0), x0 = v, x1 = v;
+  unsigned long long off0 = 0;
+  auto fetch = [&](uint32_t cc) {
+    const uint64_t ib = (uint64_t)cc * ECHUNK + (uint64_t)tid * EBPT;
+    if (ib + EBPT <= p.n) v = *(const uint4*)(p.in + ib);
+    else v = make_uint4(0, 0, 0, 0);  // tail handled by byte loads below
+    off0 = p.blk_off[cc / SCAN_BLK] + p.chunk_loc[cc];
+    if (tid == ETB - 1) {
+      const uint64_t xb = (uint64_t)(cc + 1) * ECHUNK;
+      if (xb + 2 * EBPT <= p.n) {
+        x0 = *(const uint4*)(p.in + xb);
+        x1 = *(const uint4*)(p.in + xb + EBPT);
+      }
+    }
+  };
+  if (c < p.nchunks) fetch(c);
+  for (int i = tid; i < 256; i += ETB) s_lut[i] = lutv;
   if (tid == 0) s_lut[256] = 0;
   for (int i = tid; i < EWORDS; i += ETB) s_w[i] = 0;
   for (int i = tid; i < EGAPW; i += ETB) s_g[i] = 0;
-  const unsigned long long off0 = p.blk_off[c / SCAN_BLK] + p.chunk_loc[c];
-  uint32_t b[EBPT];
-  enc_load(p.in, p.n, (uint64_t)c * ECHUNK + (uint64_t)tid * EBPT, b);
   __syncthreads();
-  uint32_t bits = 0;
+  for (uint32_t it = 0; c < p.nchunks; c += G, ++it) {
+    // this chunk's bytes (absent past n: 0x100, length 0)
+    const uint64_t ib = (uint64_t)c * ECHUNK + (uint64_t)tid * EBPT;
+    uint32_t b[EBPT];
+    if (ib + EBPT <= p.n) {
 #pragma unroll
-  for (int k = 0; k < EBPT; ++k) bits += s_lut[b[k]] & 0xFFu;
-  uint32_t cbits;
-  const uint32_t excl = enc_block_scan(bits, s_red, cbits);
-  // positions relative to B = off0 rounded down to a gap word (1024 bits): 128-bit
-  // boundaries, payload words and gap words keep their alignment, in 32 bits
-  const unsigned long long B = off0 & ~1023ull;
-  const uint32_t qs = (uint32_t)(off0 - B);  // chunk start
-  const uint32_t qend = qs + cbits;          // chunk end (the next chunk's first bit)
-  uint32_t q = qs + excl;
-  uint32_t lw = q >> 5;                      // LDS word being filled
-  int nb = (int)(q & 31);                    // pending bits in acc (the first q & 31 are zeros)
-  uint64_t acc = 0;
-  auto put = [&](uint32_t e) {
-    const uint32_t l = e & 0xFFu;
-    const uint32_t qe = q + l;
-    if ((qe ^ q) >= 128u) {  // crosses a 128-bit boundary
-      const uint32_t gv = qe & 15u;                   // nibble of segment q >> 7
-      if (gv && q < qend) atomicOr(&s_g[q >> 10], gv << (4 * ((q >> 7) & 7u)));
-    }
-    acc = (acc << l) | (e >> 8);
-    nb += (int)l;
-    if (nb >= 32) {
-      nb -= 32;
-      atomicOr(&s_w[lw], (uint32_t)(acc >> nb));
-      ++lw;
-    }
-    q = qe;
-  };
+      for (int k = 0; k < EBPT; ++k) b[k] = enc_byte(v, k);
+    } else {
 #pragma unroll
-  for (int k = 0; k < EBPT; ++k) put(s_lut[b[k]]);
-  if (tid == ETB - 1) {
-    // complete the chunk's last word with the next chunk's first symbols (their gap
-    // nibbles belong to that chunk: q >= qend skips them)
-    const uint32_t wend = (qend + 31u) & ~31u;
-    for (uint64_t i = (uint64_t)(c + 1) * ECHUNK; q < wend && i < p.n; ++i) put(s_lut[p.in[i]]);
-  }
-  if (nb > 0) atomicOr(&s_w[lw], (uint32_t)(acc << (32 - nb)));
-  __syncthreads();
-  // payload words whose first bit lies in [off0, off0 + cbits): local [w0, w1)
-  const uint32_t w0 = (qs + 31u) >> 5, w1 = (qend + 31u) >> 5;
-  uint32_t* wout = p.words + (B >> 5);
-  for (uint32_t i = w0 + tid; i < w1; i += ETB) wout[i] = s_w[i];
-  // gap words of this chunk's segments: local [0, g1]; the first and the last may
-  // hold nibbles of the neighbouring chunks
-  if (cbits) {
-    const uint32_t g1 = (qend - 1u) >> 10;
+      for (int k = 0; k < EBPT; ++k) b[k] = ib + k < p.n ? (uint32_t)p.in[ib + k] : 0x100u;
+    }
+    uint32_t xw[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+    const uint64_t xb = (uint64_t)(c + 1) * ECHUNK;
+    const bool xfull = xb + 2 * EBPT <= p.n;
+    const unsigned long long o0 = off0;
+    if (c + G < p.nchunks) fetch(c + G);  // prefetch
+    uint32_t bits = 0;
+#pragma unroll
+    for (int k = 0; k < EBPT; ++k) bits += s_lut[b[k]] & 0xFFu;
+    // block scan (double-buffered wave sums: the barrier also orders the previous
+    // iteration's write-out and re-zeroing before this iteration's OR-s)
+    uint32_t incl = bits;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += y;
+    }
+    if (lane == 63) s_red[it & 1][wid] = incl;
+    __syncthreads();
+    uint32_t before = 0, cbits = 0;
+#pragma unroll
+    for (int qq = 0; qq < ETB / 64; ++qq) {
+      const uint32_t x = s_red[it & 1][qq];
+      before += qq < wid ? x : 0u;
+      cbits += x;
+    }
+    const uint32_t excl = before + incl - bits;
+    // positions relative to B = the chunk's offset rounded down to a gap word (1024
+    // bits): 128-bit boundaries, payload words and gap words keep their alignment
+    const unsigned long long B = o0 & ~1023ull;
+    const uint32_t qs = (uint32_t)(o0 - B);  // chunk start
+    const uint32_t qend = qs + cbits;        // chunk end (the next chunk's first bit)
+    uint32_t q = qs + excl;
+    uint32_t lw = q >> 5;                    // LDS word being filled
+    int nb = (int)(q & 31);                  // pending bits in acc (the first q & 31 are zeros)
+    uint64_t acc = 0;
+    auto put = [&](uint32_t e) {
+      const uint32_t l = e & 0xFFu;
+      const uint32_t qe = q + l;
+      if ((qe ^ q) >= 128u) {  // crosses a 128-bit boundary
+        const uint32_t gv = qe & 15u;  // nibble of segment q >> 7
+        if (gv && q < qend) atomicOr(&s_g[q >> 10], gv << (4 * ((q >> 7) & 7u)));
+      }
+      acc = (acc << l) | (e >> 8);
+      nb += (int)l;
+      if (nb >= 32) {
+        nb -= 32;
+        atomicOr(&s_w[lw], (uint32_t)(acc >> nb));
+        ++lw;
+      }
+      q = qe;
+    };
+#pragma unroll
+    for (int k = 0; k < EBPT; ++k) put(s_lut[b[k]]);
+    if (tid == ETB - 1) {
+      // complete the chunk's last word with the next chunk's first symbols (their gap
+      // nibbles belong to that chunk: q >= qend skips them)
+      const uint32_t wend = (qend + 31u) & ~31u;
+      for (uint32_t k = 0; q < wend && xb + k < p.n; ++k) {
+        const uint32_t byte = xfull ? (xw[(k >> 2) & 7] >> (8 * (k & 3))) & 0xFFu : (uint32_t)p.in[xb + k];
+        put(s_lut[byte]);
+      }
+    }
+    if (nb > 0) atomicOr(&s_w[lw], (uint32_t)(acc << (32 - nb)));
+    __syncthreads();
+    // payload words whose first bit lies in [o0, o0 + cbits): local [w0, w1); the
+    // image is zeroed as it is read (up to the completion word)
+    const uint32_t w0 = (qs + 31u) >> 5, w1 = (qend + 31u) >> 5;
+    uint32_t* wout = p.words + (B >> 5);
+    for (uint32_t i = tid; i <= w1; i += ETB) {
+      const uint32_t x = s_w[i];
+      s_w[i] = 0;
+      if (i >= w0 && i < w1) wout[i] = x;
+    }
+    // gap words of this chunk's segments: local [0, g1]; the first and the last may
+    // hold nibbles of the neighbouring chunks
+    const uint32_t g1 = cbits ? (qend - 1u) >> 10 : 0u;
     uint32_t* gout = p.gaps + (B >> 10);
     for (uint32_t i = tid; i <= g1; i += ETB) {
-      const uint32_t v = s_g[i];
+      const uint32_t x = s_g[i];
+      s_g[i] = 0;
+      if (!cbits) continue;
       if (i == 0 || i == g1) {
-        if (v) atomicOr(&gout[i], v);
+        if (x) atomicOr(&gout[i], x);
       } else {
-        gout[i] = v;
+        gout[i] = x;
       }
     }
   }
@@ -423,7 +498,11 @@ extern "C" int gh_ectx_encode(gh_ectx* e, float* kernel_ms) {
   GH_EHIP(hipEventRecord(e->ev0, e->stream));
   GH_EHIP(hipMemsetAsync(e->d_gaps, 0, 4 * (GW + 4), e->stream));
   if (nchunks) {
-    hipLaunchKernelGGL(gh_enc_bits_kernel, dim3((uint32_t)nchunks), dim3(ETB), 0, e->stream, e->d_in, e->n,
+    int pb = 0, pw = 0;  // persistent grids: what is resident at once
+    GH_EHIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pb, (const void*)gh_enc_bits_kernel, ETB, 0));
+    GH_EHIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pw, (const void*)gh_enc_write_kernel, ETB, 0));
+    const uint32_t gb = (uint32_t)std::min<uint64_t>(nchunks, (uint64_t)std::max(pb, 1) * e->num_cu);
+    hipLaunchKernelGGL(gh_enc_bits_kernel, dim3(gb), dim3(ETB), 0, e->stream, e->d_in, e->n, (uint32_t)nchunks,
                        e->d_lut, e->d_chunk_bits);
     const uint32_t nblk = (uint32_t)ceil_div(nchunks, SCAN_BLK);
     uint32_t* loc = (uint32_t*)e->d_chunk_off;
@@ -431,8 +510,9 @@ extern "C" int gh_ectx_encode(gh_ectx* e, float* kernel_ms) {
     hipLaunchKernelGGL(gh_enc_scan_kernel, dim3(nblk), dim3(SCAN_TB), 0, e->stream, e->d_chunk_bits,
                        (uint32_t)nchunks, loc, blk);
     hipLaunchKernelGGL(gh_enc_blkscan_kernel, dim3(1), dim3(SCAN_TB), 0, e->stream, blk, nblk);
-    EncParams p{e->d_in, e->d_lut, loc, blk, e->d_words, e->d_gaps, e->n};
-    hipLaunchKernelGGL(gh_enc_write_kernel, dim3((uint32_t)nchunks), dim3(ETB), 0, e->stream, p);
+    EncParams p{e->d_in, e->d_lut, loc, blk, e->d_words, e->d_gaps, e->n, (uint32_t)nchunks};
+    const uint32_t gw = (uint32_t)std::min<uint64_t>(nchunks, (uint64_t)std::max(pw, 1) * e->num_cu);
+    hipLaunchKernelGGL(gh_enc_write_kernel, dim3(gw), dim3(ETB), 0, e->stream, p);
     GH_EHIP(hipGetLastError());
   }
   GH_EHIP(hipEventRecord(e->ev1, e->stream));

@@ -1,10 +1,11 @@
-// bin/encoder <input> <compressed.huff> [--threads T] [--v2]
+// bin/encoder <input> <compressed.huff> [--threads T] [--v2] [--gpu [DEVICE]]
 //
 // Drop-in for the reference encoder CLI (Huffman_coding_Gap_arrays/encoder/src/
 // huff.cpp:30-220): same positional arguments, same output format (v1 header when
 // the sizes fit the reference's 32-bit fields, the 64-bit v2 header otherwise), and
 // the same stdout lines (:176-181).  Encoding runs on the host through the gaphuff C
-// ABI (the GPU encoder is the next hot path).
+// ABI, or with --gpu on a gfx950 device (gh_ectx_*, byte-identical output; the
+// reference's own encoder is a GPU one, encoder.cu:382-457).
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -23,10 +24,11 @@ int main(int argc, char** argv) {
     std::printf("Usage: bin/encoder input output\n");
     return 1;
   }
-  int threads = 0, force = 0;
+  int threads = 0, force = 0, gpu = -1;
   for (int i = 3; i < argc; ++i) {
     if (!std::strcmp(argv[i], "--threads") && i + 1 < argc) threads = std::atoi(argv[++i]);
     else if (!std::strcmp(argv[i], "--v2")) force = 2;
+    else if (!std::strcmp(argv[i], "--gpu")) gpu = (i + 1 < argc && argv[i + 1][0] != '-') ? std::atoi(argv[++i]) : 0;
     else {
       std::fprintf(stderr, "encoder: unknown option %s\n", argv[i]);
       return 2;
@@ -47,21 +49,45 @@ int main(int argc, char** argv) {
     return 1;
   }
   std::fclose(f);
-  const double t0 = now_ms();
   gh_encode_plan* plan = new gh_encode_plan;
-  int rc = gh_encode_plan_make(in.data(), in.size(), threads, force, plan);
-  if (rc) {
-    std::fprintf(stderr, "encoder: %s\n", gh_last_error());
-    return 1;
+  std::vector<uint8_t> out;
+  double t0, t1, t2;
+  int rc;
+  if (gpu >= 0) {
+    gh_ectx* e = nullptr;
+    float ms = 0.f;
+    rc = gh_ectx_create(gpu, &e);
+    if (!rc) rc = gh_ectx_load(e, in.data(), in.size());
+    t0 = now_ms();
+    if (!rc) rc = gh_ectx_plan(e, force, plan);
+    if (!rc) rc = gh_ectx_encode(e, &ms);
+    t2 = now_ms();
+    t1 = t2 - ms;  // "kernel time": the device encode's event time
+    if (!rc) {
+      out.resize(plan->file_bytes);
+      rc = gh_ectx_download(e, out.data(), out.size());
+    }
+    if (rc) {
+      std::fprintf(stderr, "encoder: %s\n", gh_last_error());
+      return 1;
+    }
+    gh_ectx_destroy(e);
+  } else {
+    t0 = now_ms();
+    rc = gh_encode_plan_make(in.data(), in.size(), threads, force, plan);
+    if (rc) {
+      std::fprintf(stderr, "encoder: %s\n", gh_last_error());
+      return 1;
+    }
+    out.resize(plan->file_bytes);
+    t1 = now_ms();
+    rc = gh_encode_write(in.data(), plan, threads, out.data(), out.size());
+    if (rc) {
+      std::fprintf(stderr, "encoder: %s\n", gh_last_error());
+      return 1;
+    }
+    t2 = now_ms();
   }
-  std::vector<uint8_t> out(plan->file_bytes);
-  const double t1 = now_ms();
-  rc = gh_encode_write(in.data(), plan, threads, out.data(), out.size());
-  if (rc) {
-    std::fprintf(stderr, "encoder: %s\n", gh_last_error());
-    return 1;
-  }
-  const double t2 = now_ms();
   FILE* o = std::fopen(argv[2], "wb");
   if (!o) {
     std::fprintf(stderr, "Could not open output file\n");

@@ -83,3 +83,20 @@ def test_large_roundtrip(gpu):
     data = gpu.generate(77, 0.5, 100_000_000)
     img = gpu.encode_gpu(data)
     assert np.array_equal(img, gpu.encode(data))
+
+
+def test_cli_encoder_gpu(tmp_path, gpu, orc):
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    data = gpu.generate(4242, 0.9, 3_000_017)
+    data.tofile(tmp_path / "in.bin")
+    r = subprocess.run([os.path.join(root, "bin", "encoder"), str(tmp_path / "in.bin"), str(tmp_path / "c.huff"),
+                        "--gpu", "0"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "Original size: 3000017 bytes" in r.stdout
+    img = np.fromfile(tmp_path / "c.huff", dtype=np.uint8)
+    assert np.array_equal(img, orc.encode(data))
+    r = subprocess.run([os.path.join(root, "bin", "decoder"), str(tmp_path / "c.huff"), str(tmp_path / "out.bin")],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert np.array_equal(np.fromfile(tmp_path / "out.bin", dtype=np.uint8), data)
