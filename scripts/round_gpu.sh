@@ -2,7 +2,8 @@
 # Round GPU evidence on one MI355X: GPU tests, smoke(), bench lines (cfg2 default with
 # the CPU baseline, cfg3/cfg4 without), rocprofv3 kernel-trace stats of each bench
 # command, separate FETCH_SIZE / WRITE_SIZE PMC passes of each, and the per-decode
-# HBM traffic derived from them (gpurun_out/$R/pmc_traffic.json).
+# HBM traffic derived from them (gpurun_out/$R/pmc_traffic.json); then the GPU encoder's
+# numbers (scripts/bench_encode.py) and its rocprofv3 stats on cfg4.
 # Usage (from the repo root, on the box): R=r01 bash scripts/round_gpu.sh
 set -o pipefail
 R=${R:-r01}
@@ -39,4 +40,9 @@ for w in cfg2 cfg3 cfg4; do
   TR="$TR $w=$O/pmc_FETCH_SIZE_$w,$O/pmc_WRITE_SIZE_$w"
 done
 python3 scripts/pmc_traffic.py $O/pmc_traffic.json $TR > /dev/null && cat $O/pmc_traffic.json
+step encoder
+timeout -k 10 300 python scripts/bench_encode.py > $O/encode.jsonl 2> $O/encode.err || { tail $O/encode.err; exit 1; }
+cat $O/encode.jsonl
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_encode -o run \
+  -- python3 scripts/bench_encode.py cfg4 > $O/prof_encode.log 2>&1 || { tail $O/prof_encode.log; exit 1; }
 step done
