@@ -2169,6 +2169,7 @@ struct gh_ctx {
   bool ms = false;         // lean multi-symbol split kernels (gh_msplit.hip)
   bool gs = false;         // grouped single-symbol split kernels (gh_gsplit.hip)
   uint32_t ms_k = 0;       // their LUT width
+  int ms_wu = 2;           // their write kernel's chains per thread
   uint32_t ms_last_end = 0;  // end bit of the stream's last segment when the shard holds it
   uint2* d_ms_lut_c = nullptr;  // count LUT {b, end mask}
   uint2* d_ms_lut_w = nullptr;  // write LUT {symbols, b | n << 8}
@@ -2246,14 +2247,26 @@ static void free_shard(gh_ctx* c) {
 struct MsKernels {
   const void* count;
   const void* write;
+  int wu, tbw;  // write kernel: chains per thread, threads
 };
 template <int GL>
-static MsKernels ms_pair() {
-  return {(const void*)gh_ms_count_kernel<U_MS, TB_MS, GL>, (const void*)gh_ms_write_kernel<UW_MS, TBW_MS, GL>};
+static MsKernels ms_pair(int wu) {
+  if (wu == 1)
+    return {(const void*)gh_ms_count_kernel<U_MS, TB_MS, GL>, (const void*)gh_ms_write_kernel<1, MS_TILE, GL>, 1,
+            MS_TILE};
+  return {(const void*)gh_ms_count_kernel<U_MS, TB_MS, GL>, (const void*)gh_ms_write_kernel<2, MS_TILE / 2, GL>, 2,
+          MS_TILE / 2};
 }
-static MsKernels ms_kernels(uint32_t K) {
+// Write-kernel chains per thread: one (512 threads) for LUTs of up to 10 bits, two
+// otherwise (measured: cfg2, K=10, 120 vs 127 us; cfg3, K=11, 675 vs 655 us).
+// GH_MS_WU=1|2 overrides.
+static int ms_write_chains(uint32_t K) {
+  if (const char* e = getenv("GH_MS_WU")) return atoi(e) == 1 ? 1 : 2;
+  return K <= 10 ? 1 : 2;
+}
+static MsKernels ms_kernels(uint32_t K, int wu) {
   const int g = ms_group(K);
-  return g >= 4 ? ms_pair<4>() : g == 3 ? ms_pair<3>() : ms_pair<2>();
+  return g >= 4 ? ms_pair<4>(wu) : g == 3 ? ms_pair<3>(wu) : ms_pair<2>(wu);
 }
 
 // Lean multi-symbol split kernels: LUTs, geometry, buffers (gh_msplit.hip).
@@ -2297,10 +2310,11 @@ static int ms_setup(gh_ctx* c) {
   // Staging: the most workgroups per CU (8 .. 1) whose staging still holds one
   // chain's worst case (TB_MS segments x maxsyms); a tile that exceeds it is staged
   // one chain at a time (gh_ms_write_kernel).
-  constexpr int NW = TBW_MS / 64;
-  const size_t misc = 4 * (UW_MS * NW + 2) + 8 * NW;
-  const size_t chain_worst = (size_t)TBW_MS * maxsyms + 64 + 32;
-  const size_t full_worst = (size_t)UW_MS * TBW_MS * maxsyms + 64 + 32;
+  const MsKernels mk = ms_kernels(K, ms_write_chains(K));
+  const int NW = mk.tbw / 64;
+  const size_t misc = 4 * (mk.wu * NW + 2) + 8 * NW;
+  const size_t chain_worst = (size_t)mk.tbw * maxsyms + 64 + 32;
+  const size_t full_worst = (size_t)mk.wu * mk.tbw * maxsyms + 64 + 32;
   size_t stage = 0;
   for (int wg = 8; wg >= 1 && stage == 0; --wg) {
     const long avail = (long)(163840 / wg) - (long)lb - (long)misc;
@@ -2313,9 +2327,9 @@ static int ms_setup(gh_ctx* c) {
   c->lds = lb + c->stage_bytes + misc;
   c->lds_count = std::max<size_t>(lb, 64);
   int pc_c = 0, pc_w = 0;
-  const MsKernels mk = ms_kernels(K);
+  c->ms_wu = mk.wu;
   GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc_c, mk.count, TB_MS, c->lds_count));
-  GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc_w, mk.write, TBW_MS, c->lds));
+  GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc_w, mk.write, mk.tbw, c->lds));
   if (pc_c < 1 || pc_w < 1) return fail(GH_E_HIP, "msplit kernels do not fit on a CU");
   c->grid = (uint32_t)std::min<uint64_t>(c->ntiles, (uint64_t)pc_w * c->num_cu);
   // count ranges nest in write ranges (floor(b*n/grid) boundaries coincide for
@@ -2909,9 +2923,9 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     mw.lut = c->d_ms_lut_w;
     ac[0] = &mc;
     aw[0] = &mw;
-    const MsKernels mk = ms_kernels(c->ms_k);
+    const MsKernels mk = ms_kernels(c->ms_k, c->ms_wu);
     GH_HIP(hipLaunchKernel(mk.count, dim3(c->grid * c->count_per), dim3(TB_MS), ac, c->lds_count, st));
-    GH_HIP(hipLaunchKernel(mk.write, dim3(c->grid), dim3(TBW_MS), aw, c->lds, st));
+    GH_HIP(hipLaunchKernel(mk.write, dim3(c->grid), dim3(mk.tbw), aw, c->lds, st));
   } else if (c->tile) {
     TileParams t{};
     t.payload = c->d_payload;

@@ -38,11 +38,9 @@
 
 constexpr int TB_MS = 256;  // workgroup size of both kernels
 constexpr int U_MS = 2;     // segments per thread (lock-step chains), count kernel
-#ifndef GH_MS_WU
-#define GH_MS_WU 2
-#endif
-// write kernel: UW_MS chains per thread, TBW_MS threads, the same 512-segment tiles
-constexpr int UW_MS = GH_MS_WU, TBW_MS = U_MS * TB_MS / GH_MS_WU;
+// write kernel: 1 or 2 chains per thread (512 or 256 threads), the same 512-segment
+// tiles; the host picks per LUT width (ms_write_chains)
+constexpr int MS_TILE = U_MS * TB_MS;
 // lookups per funnel shift: G * K <= 31 (template parameter GL of the kernels)
 inline int ms_group(uint32_t K) { return K <= 7 ? 4 : K <= 10 ? 3 : 2; }
 

@@ -224,11 +224,15 @@ def test_graft_smoke(gpu):
 
 @pytest.mark.parametrize("k", ["", "10", "11", "12"])
 @pytest.mark.parametrize("stage", ["", "1"])
-def test_lean_split_widths_and_staging(gpu, orc, k, stage, monkeypatch):
+@pytest.mark.parametrize("wu", ["", "1", "2"])
+def test_lean_split_widths_and_staging(gpu, orc, k, stage, wu, monkeypatch):
     """The lean multi-symbol split kernels (gh_msplit.hip) at every LUT width, with the
     default staging and with the staging forced down to one chain's worst case, so
-    that tiles are staged one chain at a time (GH_MS_STAGE)."""
+    that tiles are staged one chain at a time (GH_MS_STAGE), and with either write
+    geometry (GH_MS_WU: one chain per thread x 512, or two x 256)."""
     monkeypatch.setenv("GH_MODE", "msplit")
+    if wu:
+        monkeypatch.setenv("GH_MS_WU", wu)
     if k:
         monkeypatch.setenv("GH_MS_K", k)
     if stage:
