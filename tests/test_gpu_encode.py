@@ -100,3 +100,9 @@ def test_cli_encoder_gpu(tmp_path, gpu, orc):
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert np.array_equal(np.fromfile(tmp_path / "out.bin", dtype=np.uint8), data)
+
+
+def test_empty_input(gpu, orc):
+    img = gpu.encode_gpu(np.zeros(0, dtype=np.uint8))
+    assert np.array_equal(img, gpu.encode(b""))
+    assert gpu.decode(img).size == 0
