@@ -2477,6 +2477,12 @@ extern "C" int gh_ctx_create(int device, gh_ctx** out) {
   return GH_OK;
 }
 
+extern "C" int gh_ctx_device(gh_ctx* c, int* device) {
+  if (!c || !device) return fail(GH_E_ARG, "null argument");
+  *device = c->device;
+  return GH_OK;
+}
+
 extern "C" int gh_ctx_destroy(gh_ctx* c) {
   if (!c) return GH_OK;
   (void)hipSetDevice(c->device);

@@ -46,7 +46,7 @@ EXPORTED = (
     "gh_ctx_output", "gh_ctx_copy_output", "gh_ctx_reset_timing", "gh_decode", "gh_plan_shards",
     "gh_device_count", "gh_version", "gh_last_error",
     "gh_ectx_create", "gh_ectx_destroy", "gh_ectx_load", "gh_ectx_plan", "gh_ectx_encode",
-    "gh_ectx_download",
+    "gh_ectx_download", "gh_ctx_device", "gh_sync_gaps", "gh_ctx_load_raw",
 )
 
 
@@ -85,6 +85,11 @@ class gh_report(ctypes.Structure):
         ("mode", ctypes.c_uint32), ("path", ctypes.c_uint32),
         ("slow_lookbacks", ctypes.c_uint64),
     ]
+
+
+class gh_sync_report(ctypes.Structure):
+    _fields_ = [("g", ctypes.c_uint64), ("mismatches", ctypes.c_uint64), ("passes", ctypes.c_uint32),
+                ("kernel_ms", ctypes.c_float)]
 
 
 MODE_NAMES = {0: "fused", 1: "split", 2: "tile"}
@@ -134,6 +139,9 @@ def lib() -> ctypes.CDLL:
             "gh_ectx_plan": ([P, I, ctypes.POINTER(gh_encode_plan)], I),
             "gh_ectx_encode": ([P, ctypes.POINTER(ctypes.c_float)], I),
             "gh_ectx_download": ([P, P, U64], I),
+            "gh_ctx_device": ([P, ctypes.POINTER(I)], I),
+            "gh_sync_gaps": ([I, P, U32, P, U64, P, P, ctypes.POINTER(gh_sync_report)], I),
+            "gh_ctx_load_raw": ([P, P, U32, U64, P, U64, U64, ctypes.POINTER(gh_sync_report)], I),
             "gh_version": ([], ctypes.c_char_p),
             "gh_last_error": ([], ctypes.c_char_p),
         }
@@ -332,6 +340,18 @@ class Decoder:
         self._stream = stream
         _check(lib().gh_ctx_load(self._h, ctypes.byref(stream.c), seg_begin, seg_end, out_cap))
 
+    def load_raw(self, symbols: Sequence[tuple], n: int, units, out_cap: int = 0) -> gh_sync_report:
+        """Load a raw (gap-less) stream: u32 ``units``, canonical ``symbols`` list
+        [(symbol, length)] in code order, ``n`` output bytes.  The gap array is
+        built on the GPU (gh_sync_gaps); returns its report."""
+        u = np.ascontiguousarray(units, dtype=np.uint32)
+        sy = _syms(symbols)
+        r = gh_sync_report()
+        _check(lib().gh_ctx_load_raw(self._h, ctypes.byref(sy), len(symbols), n, _ptr(u), u.size, out_cap,
+                                     ctypes.byref(r)))
+        self._stream = None
+        return r
+
     def decode(self, hip_stream: int = 0, timed: bool = True) -> None:
         _check(lib().gh_ctx_decode(self._h, ctypes.c_void_p(hip_stream or None), int(timed)))
 
@@ -374,6 +394,38 @@ def decode(file_bytes, ngpus: int = 1, devices: Optional[Sequence[int]] = None,
     r = gh_report()
     _check(lib().gh_decode(ctypes.byref(s.c), _ptr(out), out.size, ctypes.byref(o), ctypes.byref(r)))
     return out[: s.n]
+
+
+def _syms(symbols: Sequence[tuple]):
+    arr = (gh_sym * max(1, len(symbols)))()
+    for i, (sy, ln) in enumerate(symbols):
+        arr[i].symbol, arr[i].length = sy, ln
+    return arr
+
+
+def sync_gaps(symbols: Sequence[tuple], d_words: int, w: int, d_gap_words: int, device: int = 0,
+              hip_stream: int = 0) -> gh_sync_report:
+    """Gap words of a device-resident raw stream (device addresses as ints, e.g. a
+    torch tensor's data_ptr()); see gh_sync_gaps in include/gaphuff.h."""
+    sy = _syms(symbols)
+    r = gh_sync_report()
+    _check(lib().gh_sync_gaps(device, ctypes.byref(sy), len(symbols), ctypes.c_void_p(d_words), w,
+                              ctypes.c_void_p(d_gap_words), ctypes.c_void_p(hip_stream or None),
+                              ctypes.byref(r)))
+    return r
+
+
+def decode_raw(units, symbols: Sequence[tuple], n: int, device: int = 0) -> np.ndarray:
+    """Self-synchronising decode of a raw stream: the role of CUHD's
+    CUHDGPUDecoder::decode (gpuhd/include/cuhd_gpu_decoder.h:24-32) for u32 units
+    packed MSB-first (llhuffman_encoder.cc:200-238).  Returns the n decoded bytes."""
+    with Decoder(device) as d:
+        d.load_raw(symbols, n, units)
+        d.decode(timed=False)
+        rep = d.report()
+        if rep.status:
+            raise GapHuffError(-7, f"device status {rep.status}")
+        return d.download(n) if n else np.zeros(0, dtype=np.uint8)
 
 
 def decoder_l1_l2(input_words, inputfilesize: int, outputfilesize: int, gap_element_num: int,

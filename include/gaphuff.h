@@ -197,6 +197,36 @@ int gh_ctx_copy_output(gh_ctx* ctx, uint64_t byte_offset, void* dst, uint64_t nb
 /* Reset the accumulated kernel timing. */
 int gh_ctx_reset_timing(gh_ctx* ctx);
 
+/* HIP device ordinal the context is bound to. */
+int gh_ctx_device(gh_ctx* ctx, int* device);
+
+/* ---- self-synchronising decode of gap-less streams ---- */
+/* Replaces CUHD's decoder for raw Huffman streams without a gap array
+ * (gpuhd/src/cuhd_gpu_decoder.cu:145-523, CUHDGPUDecoder::decode declared at
+ * gpuhd/include/cuhd_gpu_decoder.h:24-32; stream = u32 units, codewords MSB-first,
+ * llhuffman_encoder.cc:200-238).  The GPU finds every 128-bit segment's first
+ * codeword start by decoding from arbitrary bits and verifying that neighbouring
+ * walks agree (repairing where they do not), which yields the gap array; the stream
+ * is then decoded by the gap-array kernels.  Codes: the canonical (symbol,length)
+ * list in file order (lengths 1..16, non-decreasing), as in gh_stream. */
+typedef struct gh_sync_report {
+  uint64_t g;           /* 128-bit segments = ceil(w / 4)                          */
+  uint64_t mismatches;  /* segment boundaries the first walk got wrong (repaired)  */
+  uint32_t passes;      /* verify/repair passes (1 when the first walk was right)  */
+  float kernel_ms;      /* sync walk + first verify pass, HIP events               */
+} gh_sync_report;
+/* Gap words (ceil(ceil(w/4)/8) u32, the gap-array file's layout) of the raw stream
+ * d_words[0..w) (device memory, 16-byte aligned) into d_gap_words on `hip_stream`
+ * (NULL = default stream) of `device`.  Synchronous (the verify loop reads a
+ * counter back).  rep may be NULL. */
+int gh_sync_gaps(int device, const gh_sym* syms, uint32_t nsyms, const uint32_t* d_words,
+                 uint64_t w, uint32_t* d_gap_words, void* hip_stream, gh_sync_report* rep);
+/* gh_ctx_load for a raw stream held in host memory: uploads words[0..w), builds its
+ * gap array with gh_sync_gaps and loads the whole stream (n output bytes) into ctx;
+ * gh_ctx_decode / gh_ctx_report / gh_ctx_download then work as for a gap-array file. */
+int gh_ctx_load_raw(gh_ctx* ctx, const gh_sym* syms, uint32_t nsyms, uint64_t n,
+                    const uint32_t* words, uint64_t w, uint64_t out_cap, gh_sync_report* rep);
+
 /* One-shot decode of a whole stream into host memory `out` (out_len >= N):
  * mirrors decoder_l1_l2 (decoder.cu:732-815) without its 200-iteration loop.
  * ngpus <= 0 or 1: device `devices ? devices[0] : 0`; ngpus > 1 shards the

@@ -213,3 +213,106 @@ def run_reference_cpu(name: str, data: np.ndarray, timeout: float = 600.0) -> di
                 "threads": threads, "wall_s": wall}
     finally:
         shutil.rmtree(td, ignore_errors=True)
+
+
+# ------------------------------------------------------- raw (gap-less) streams
+# Restatement of the self-synchronising decoder's stream (gpuhd, SURVEY.md §8(f)
+# rank 3): llhuffman_encoder.cc:173-198 (canonical codes in list order),
+# :200-238 (codewords packed MSB-first into u32 units).  Test infrastructure only.
+def canonical_codes(syms) -> list:
+    """Codes of a (symbol, length) list in list order: llhuffman_encoder.cc:181-193,
+    identical to package_merge.cpp:168-181 (code = (code+1) << (len' - len))."""
+    codes, code = [], 0
+    for i, (_, ln) in enumerate(syms):
+        if i:
+            code = (code + 1) << (ln - syms[i - 1][1])
+        codes.append(code)
+    return codes
+
+
+def _code_arrays(data, syms):
+    d = _u8(data)
+    code = np.zeros(256, dtype=np.uint64)
+    ln = np.zeros(256, dtype=np.uint64)
+    for (s, l), c in zip(syms, canonical_codes(syms)):
+        code[s], ln[s] = c, l
+    if d.size and np.any(ln[d] == 0):
+        raise ValueError("data holds a symbol outside the table")
+    return d, code[d], ln[d]
+
+
+def raw_encode(data, syms) -> np.ndarray:
+    """u32 units of the raw stream (bit 0 = bit 31 of unit 0; the last unit
+    zero-padded, where encode_memory's final unit is undefined, :228-232)."""
+    d, c, l = _code_arrays(data, syms)
+    bits = int(l.sum())
+    w = (bits + 31) // 32
+    out = np.zeros(w * 32 + 64, dtype=np.uint8)
+    if d.size:
+        ends = np.cumsum(l)
+        starts = ends - l
+        for k in range(16):  # bit k (from the MSB) of every codeword
+            m = l > k
+            pos = (starts[m] + k).astype(np.int64)
+            out[pos] = ((c[m] >> (l[m] - 1 - k)) & 1).astype(np.uint8)
+    return np.packbits(out[: w * 32]).view(">u4").astype(np.uint32)
+
+
+def raw_gaps(data, syms) -> np.ndarray:
+    """Gap words of the raw stream: entry of segment j+1 (first codeword start at
+    or after 128(j+1)) minus 128(j+1) in nibble j, 8 per u32 LSB-first; the last
+    nibble is 0 (encoder.cu:307-312,358-379)."""
+    d, _, l = _code_arrays(data, syms)
+    bits = int(l.sum())
+    g = ((bits + 31) // 32 + 3) // 4
+    nib = np.zeros(8 * ((g + 7) // 8), dtype=np.uint32)
+    if g > 1:
+        starts = np.cumsum(l) - l
+        bnd = 128 * np.arange(1, g, dtype=np.uint64)
+        idx = np.searchsorted(starts, bnd)
+        entry = np.where(idx < starts.size, starts[np.minimum(idx, starts.size - 1)], bnd)
+        nib[: g - 1] = (entry - bnd).astype(np.uint32)
+    nib = nib.reshape(-1, 8) << (4 * np.arange(8, dtype=np.uint32))
+    return np.bitwise_or.reduce(nib, axis=1).astype(np.uint32) if nib.size else np.zeros(0, np.uint32)
+
+
+def raw_decode(units, syms, n: int) -> np.ndarray:
+    """Bit-serial decode of n symbols (small cases only): the per-codeword table
+    walk of cuhd_gpu_decoder.cu:86-118 run from bit 0."""
+    by_code = {(l, c): s for (s, l), c in zip(syms, canonical_codes(syms))}
+    bits = np.unpackbits(np.asarray(units, dtype=np.uint32).astype(">u4").view(np.uint8))
+    out = np.zeros(n, dtype=np.uint8)
+    pos = 0
+    for i in range(n):
+        c = 0
+        for l in range(1, 17):
+            c = (c << 1) | int(bits[pos + l - 1]) if pos + l - 1 < bits.size else c << 1
+            if (l, c) in by_code:
+                out[i] = by_code[(l, c)]
+                pos += l
+                break
+        else:
+            raise RuntimeError(f"invalid code at bit {pos}")
+    return out
+
+
+def ref_llhuff(data):
+    """Reference raw-stream encoder (gpuhd/encoder, compiled into _ref/llhuff_driver):
+    returns (syms in code order, units)."""
+    exe = os.path.join(REF, "llhuff_driver")
+    with tempfile.TemporaryDirectory() as td:
+        fi, fo = os.path.join(td, "in.bin"), os.path.join(td, "out.llh")
+        _u8(data).tofile(fi)
+        subprocess.run([exe, fi, fo], check=True, capture_output=True)
+        return read_llh(open(fo, "rb").read())
+
+
+def read_llh(b: bytes):
+    """Parse the llhuff_driver output: u32 nsyms, {u8 sym, u8 len}*, u64 units, units."""
+    ns = int(np.frombuffer(b[:4], "<u4")[0])
+    e = np.frombuffer(b[4 : 4 + 2 * ns], np.uint8).reshape(-1, 2)
+    syms = [(int(s), int(l)) for s, l in e]
+    o = 4 + 2 * ns
+    nu = int(np.frombuffer(b[o : o + 8], "<u8")[0])
+    units = np.frombuffer(b[o + 8 : o + 8 + 4 * nu], "<u4").astype(np.uint32)
+    return syms, units

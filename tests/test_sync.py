@@ -1,0 +1,217 @@
+"""Self-synchronising decode of gap-less (raw) streams — SURVEY.md §8(f) rank 3.
+
+Reference: gpuhd's CUHD decoder (gpuhd/src/cuhd_gpu_decoder.cu:145-523) over raw u32
+units from the LLHuff encoder (gpuhd/encoder/src/llhuffman_encoder.cc:200-238).
+CPU tests pin the oracle's raw-stream restatement (oracle.raw_encode / raw_gaps /
+raw_decode) against the REFERENCE encoder's own output (tests/golden/*.llh, made by
+tests/golden/make_llhuff_golden.py from oracle/_ref/llhuff_driver) and against the
+gap-array encoder.  GPU tests call the C ABI (gh_sync_gaps, gh_ctx_load_raw) and
+compare bit-exactly with the oracle.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+LLH = json.load(open(os.path.join(GOLD, "llhuff.json")))
+
+
+def _llh(name):
+    import oracle
+    return oracle.read_llh(open(os.path.join(GOLD, name + ".llh"), "rb").read())
+
+
+def _bin(name):
+    return np.fromfile(os.path.join(GOLD, name + ".bin"), dtype=np.uint8)
+
+
+# ------------------------------------------------------------------------- CPU
+@pytest.mark.parametrize("name", sorted(LLH))
+def test_llhuff_golden_units_reproduced(orc, name):
+    """The oracle's packing == the reference encode_memory units (all but the last
+    unit, which encode_memory leaves undefined when the data ends mid-unit)."""
+    import hashlib
+    b = open(os.path.join(GOLD, name + ".llh"), "rb").read()
+    assert hashlib.sha256(b).hexdigest() == LLH[name]["sha256"]
+    syms, units = _llh(name)
+    data = _bin(name)
+    mine = orc.raw_encode(data, syms)
+    if len(syms) == 1:
+        # reference defect: get_symbol_lengths leaves Symbol::count unset for a
+        # one-symbol input (llhuffman_encoder.cc:39-47), so compressed_size is 0
+        assert units.size == 0 and not mine.any()
+        return
+    assert mine.size == units.size == LLH[name]["units"]
+    assert np.array_equal(mine[:-1], units[:-1])
+
+
+@pytest.mark.parametrize("name", sorted(LLH))
+def test_llhuff_golden_decodes(orc, name):
+    syms, units = _llh(name)
+    data = _bin(name)
+    assert np.array_equal(orc.raw_decode(units, syms, data.size), data)
+
+
+def test_llhuff_reference_live(orc):
+    if not orc.ref_available("llhuff_driver"):
+        pytest.skip("reference raw encoder not built (no /root/reference)")
+    for seed, r in ((11, 0.3), (12, 0.95), (13, 0.05)):
+        d = orc.generate(seed, r, 30011)
+        syms, units = orc.ref_llhuff(d)
+        assert max(l for _, l in syms) <= 11  # CUHD's MAX_CODEWORD_LENGTH
+        assert np.array_equal(orc.raw_encode(d, syms)[:-1], units[:-1])
+
+
+@pytest.mark.parametrize("r,n", [(0.5, 20000), (0.9, 20000), (0.1, 3000), (0.999, 50000), (0.5, 7),
+                                 (0.5, 1)])
+def test_raw_stream_is_gap_array_payload(orc, gh, r, n):
+    """A gap-array file's payload is the raw stream of its code, and its gap words are
+    the raw stream's segment entries (so the GPU's synthesised gaps have a fixed
+    expected value)."""
+    import ctypes
+    d = orc.generate(1, r, n)
+    s = gh.parse(orc.encode(d))
+    nw = (s.g + 7) // 8
+    gw = np.ctypeslib.as_array(ctypes.cast(s.c.gap_words, ctypes.POINTER(ctypes.c_uint32)), (max(nw, 1),))[:nw]
+    pw = np.ctypeslib.as_array(ctypes.cast(s.c.payload, ctypes.POINTER(ctypes.c_uint32)), (max(s.w, 1),))[:s.w]
+    assert np.array_equal(orc.raw_gaps(d, s.symbols), gw)
+    assert np.array_equal(orc.raw_encode(d, s.symbols), pw)
+
+
+def test_desync_table_oracle(orc):
+    """The adversarial stream of the GPU repair test: a 1-bit code plus four 3-bit
+    codes, data all '111' — a walk that starts off the 3-bit phase never resyncs."""
+    syms = [(0, 1), (1, 3), (2, 3), (3, 3), (4, 3)]
+    d = np.full(1000, 4, dtype=np.uint8)
+    u = orc.raw_encode(d, syms)
+    assert np.all(u[:-1] == 0xFFFFFFFF)
+    assert np.array_equal(orc.raw_decode(u, syms, d.size), d)
+
+
+def test_sync_abi_exports(gh):
+    L = gh.lib()
+    for name in ("gh_sync_gaps", "gh_ctx_load_raw", "gh_ctx_device"):
+        assert hasattr(L, name)
+
+
+# ------------------------------------------------------------------------- GPU
+def _hip():
+    """The HIP runtime libgaphuff itself links (torch bundles another one, and two
+    runtimes in one process do not share the device)."""
+    import ctypes
+    L = ctypes.CDLL("/opt/rocm/lib/libamdhip64.so")
+    L.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+    L.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    L.hipFree.argtypes = [ctypes.c_void_p]
+    return L
+
+
+def _sync_on_gpu(gh, units, syms):
+    import ctypes
+    H = _hip()
+    w = int(units.size)
+    g = (w + 3) // 4
+    nw = (g + 7) // 8
+    src = np.concatenate([units, np.zeros(4, np.uint32)]).astype(np.uint32)
+    gaps = np.full(nw + 4, 0xFFFFFFFF, dtype=np.uint32)
+    dw, dg = ctypes.c_void_p(), ctypes.c_void_p()
+    assert H.hipMalloc(ctypes.byref(dw), src.nbytes) == 0
+    assert H.hipMalloc(ctypes.byref(dg), gaps.nbytes) == 0
+    try:
+        assert H.hipMemcpy(dw, src.ctypes.data, src.nbytes, 1) == 0  # H2D
+        assert H.hipMemcpy(dg, gaps.ctypes.data, gaps.nbytes, 1) == 0
+        rep = gh.sync_gaps(syms, dw.value, w, dg.value, device=0)
+        assert H.hipMemcpy(gaps.ctypes.data, dg, gaps.nbytes, 2) == 0  # D2H
+    finally:
+        H.hipFree(dw)
+        H.hipFree(dg)
+    assert np.all(gaps[nw:] == 0xFFFFFFFF), "wrote past the gap words"
+    return gaps[:nw], rep
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("r,n", [(0.5, 1), (0.5, 7), (0.5, 20000), (0.9, 300007), (0.1, 300007),
+                                 (0.999, 1 << 20), (0.0, 65536), (1.0, 4096)])
+def test_gpu_sync_gaps_match_oracle(gpu, orc, r, n):
+    d = orc.generate(7, r, n)
+    syms = orc.symbols_of(d)
+    units = orc.raw_encode(d, syms)
+    gaps, rep = _sync_on_gpu(gpu, units, syms)
+    assert rep.g == (units.size + 3) // 4
+    assert np.array_equal(gaps, orc.raw_gaps(d, syms))
+
+
+@pytest.mark.gpu
+def test_gpu_sync_long_codes(gpu, orc):
+    """Codes of 13-16 bits (the threshold path) from the geometric fixture."""
+    d = _bin("geometric_long_codes")
+    syms = orc.symbols_of(d)
+    assert max(l for _, l in syms) > 12
+    units = orc.raw_encode(d, syms)
+    gaps, _ = _sync_on_gpu(gpu, units, syms)
+    assert np.array_equal(gaps, orc.raw_gaps(d, syms))
+    assert np.array_equal(gpu.decode_raw(units, syms, d.size), d)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(LLH))
+def test_gpu_decode_reference_llhuff_streams(gpu, name):
+    """Streams written by the REFERENCE raw encoder decode to the input."""
+    syms, units = _llh(name)
+    data = _bin(name)
+    if units.size == 0:  # the reference's one-symbol defect: an empty, truncated stream
+        with pytest.raises(gpu.GapHuffError):
+            gpu.decode_raw(units, syms, data.size)
+        return
+    assert np.array_equal(gpu.decode_raw(units, syms, data.size), data)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("r", [0.1, 0.5, 0.9])
+def test_gpu_decode_raw_roundtrip(gpu, orc, r):
+    d = orc.generate(21, r, 3_000_017)
+    syms = orc.symbols_of(d)
+    units = orc.raw_encode(d, syms)
+    with gpu.Decoder(0) as dec:
+        rep = dec.load_raw(syms, d.size, units)
+        dec.decode()
+        out = dec.download(d.size)
+        assert dec.report().status == 0
+    assert rep.passes >= 1
+    assert np.array_equal(out, d)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,stride", [(100_000, 0), (40_000, 997)])
+def test_gpu_sync_repairs_desync(gpu, orc, n, stride):
+    """Adversarial code whose walks never resynchronise on their own: the verify pass
+    must find the mismatches and the repair chains must fix every boundary."""
+    syms = [(0, 1), (1, 3), (2, 3), (3, 3), (4, 3)]
+    d = np.full(n, 4, dtype=np.uint8)
+    if stride:
+        d[::stride] = 0  # an occasional 1-bit codeword shifts the phase
+    units = orc.raw_encode(d, syms)
+    gaps, rep = _sync_on_gpu(gpu, units, syms)
+    assert rep.mismatches > 0 and rep.passes >= 2
+    assert np.array_equal(gaps, orc.raw_gaps(d, syms))
+    assert np.array_equal(gpu.decode_raw(units, syms, d.size), d)
+
+
+@pytest.mark.gpu
+def test_gpu_decode_raw_empty(gpu):
+    with gpu.Decoder(0) as dec:
+        rep = dec.load_raw([(65, 1)], 0, np.zeros(0, np.uint32))
+        assert rep.g == 0
+    assert gpu.decode_raw(np.zeros(0, np.uint32), [(65, 1)], 0).size == 0
+
+
+@pytest.mark.gpu
+def test_gpu_decode_raw_large_property(gpu, orc):
+    """64 MiB r=0.1 stream: decode == input (size-independent round trip)."""
+    d = gpu.generate(5, 0.1, 1 << 26)
+    s = gpu.parse(gpu.encode(d))
+    import ctypes
+    pw = np.ctypeslib.as_array(ctypes.cast(s.c.payload, ctypes.POINTER(ctypes.c_uint32)), (s.w,))
+    assert np.array_equal(gpu.decode_raw(pw.copy(), s.symbols, d.size), d)
