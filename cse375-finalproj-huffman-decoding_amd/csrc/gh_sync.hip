@@ -19,9 +19,11 @@
 // kernels unchanged; the count pass, scan and write pass are the hot path's own.
 //
 //  gh_sync_kernel      thread t starts decoding at the raw bit 128t (possibly
-//                      mid-codeword) and walks 256 bits.  a_t = its entry offset at
-//                      128(t+1) (the candidate gap[t]); b_t = its entry offset at
-//                      128(t+2).  Writes gap words and pairs[t] = a_t | b_t << 4.
+//                      mid-codeword); walks of neighbouring threads then advance in
+//                      lock-step until they merge (below).  a_t = the entry offset
+//                      at 128(t+1) (the candidate gap[t]); b_t = the entry offset at
+//                      128(t+2) on the same walk.  Writes gap words and
+//                      pairs[t] = a_t | b_t << 4.
 //  gh_sync_fix_kernel  verification: b_t == a_{t+1} for every t proves every a_t
 //                      (induction: thread 0 starts at the true bit 0; if a_t is on
 //                      the true path then thread t's walk is true from there, so b_t
@@ -53,6 +55,7 @@ namespace {
 constexpr int SK = 12;          // LUT prefix bits
 constexpr int SYNC_TB = 256;    // threads per workgroup
 constexpr uint32_t SYNC_CHAIN = 256;  // segments one repair chain may walk per pass
+constexpr int SYNC_HALO = 16;         // warm-up segments per wave (GH_SYNC_HALO overrides)
 
 #define GH_HIPS(expr)                                                             \
   do {                                                                            \
@@ -70,7 +73,10 @@ struct SyncParams {
   uint32_t* gaps;         // ceil(g / 8) gap words
   uint32_t* pairs;        // g bytes {a | b << 4}, as words
   unsigned int* counter;  // mismatches found by a fix pass
+  uint32_t halo;          // warm-up segments per wave (multiple of 8, < 64)
 };
+
+__device__ __forceinline__ uint64_t ceil_div_d(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 
 __device__ __forceinline__ uint32_t ld_word(const uint32_t* w, uint64_t nw, uint64_t i) {
   return i < nw ? w[i] : 0u;
@@ -107,49 +113,106 @@ __device__ __forceinline__ void stage_lut(uint16_t* lds, const uint16_t* g) {
   __syncthreads();
 }
 
+// Walk segment j (words 4j..4j+4) from entry offset `off`; returns the entry offset at
+// boundary 128(j+1).
+__device__ __forceinline__ uint32_t walk_segment(uint64_t j, uint32_t off, const uint16_t* lut,
+                                                 const SyncParams& p) {
+  const uint64_t w0 = 4 * j;
+  uint32_t w[5];
+  if (w0 + 5 <= p.w) {
+    const uint4 x = *reinterpret_cast<const uint4*>(p.words + w0);
+    w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w;
+    w[4] = p.words[w0 + 4];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) w[i] = ld_word(p.words, p.w, w0 + i);
+  }
+  off = walk_word<false>(w[0], w[1], off, lut, p);
+  off = walk_word<false>(w[1], w[2], off, lut, p);
+  off = walk_word<false>(w[2], w[3], off, lut, p);
+  return walk_word<true>(w[3], w[4], off, lut, p);
+}
+
+// Each wavefront owns `out` = 64 - halo consecutive output segments [wo, wo+out); its
+// lanes walk segments [wo-halo, wo+out), so the first `halo` lanes are warm-up walks
+// that overlap the previous wave's segments.  Lane i's walk starts at the raw bit 128t
+// (t = wo-halo+i, possibly mid-codeword) and records its entry at boundary t+1.  Then,
+// in lock-step rounds (CUHD phase 1's scheme, cuhd_gpu_decoder.cu:186-229, here per
+// wavefront so no workgroup barrier is needed: a wave's LDS operations complete in
+// issue order), every walk that has not merged goes one segment on and compares its
+// entry with the record its right neighbour's walk left there: equal means the two
+// walks coincide from here on, so it stops; otherwise it overwrites the record (the
+// lower walk started earlier, so it is the one to keep).  Walks stop at boundary
+// wo+out+1 (the last b the wave needs).  The halo makes the wave's first output entry
+// come from a walk that started `halo` segments (128*halo bits) earlier, which on
+// ordinary codes has long merged with the true path, so the verify pass rarely finds a
+// seam to repair.
+constexpr int SYNC_WAVE = 64;
 __global__ __launch_bounds__(SYNC_TB) void gh_sync_kernel(SyncParams p) {
   __shared__ uint16_t lut[1 << SK];
+  __shared__ uint8_t rec_all[SYNC_TB / SYNC_WAVE][SYNC_WAVE + 4];
   stage_lut(lut, p.lut);
-  const uint64_t stride = (uint64_t)gridDim.x * SYNC_TB;
-  for (uint64_t base = (uint64_t)blockIdx.x * SYNC_TB; base < p.g; base += stride) {
-    const uint64_t t = base + threadIdx.x;
-    uint32_t a = 0, b = 0;
-    if (t < p.g) {
-      uint32_t w[9];
-      const uint64_t w0 = 4 * t;
-      if (w0 + 9 <= p.w) {
-        const uint4 x = *reinterpret_cast<const uint4*>(p.words + w0);
-        const uint4 y = *reinterpret_cast<const uint4*>(p.words + w0 + 4);
-        w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w;
-        w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
-        w[8] = p.words[w0 + 8];
-      } else {
-#pragma unroll
-        for (int i = 0; i < 9; ++i) w[i] = ld_word(p.words, p.w, w0 + i);
+  const uint32_t lane = threadIdx.x % SYNC_WAVE;
+  const uint32_t halo = p.halo, out = SYNC_WAVE - halo;
+  volatile uint8_t* rec = rec_all[threadIdx.x / SYNC_WAVE];
+  const uint64_t nwaves = ceil_div_d(p.g, out);
+  const uint64_t wstride = (uint64_t)gridDim.x * (SYNC_TB / SYNC_WAVE);
+  for (uint64_t wv = (uint64_t)blockIdx.x * (SYNC_TB / SYNC_WAVE) + threadIdx.x / SYNC_WAVE; wv < nwaves;
+       wv += wstride) {
+    const int64_t w0 = (int64_t)(wv * out) - (int64_t)halo;  // segment of lane 0
+    const int64_t ts = w0 + (int64_t)lane;
+    const uint64_t t = (uint64_t)ts;
+    const uint64_t kcap = (uint64_t)(w0 + SYNC_WAVE);  // last segment walked: boundary w0+65
+    bool active = ts >= 0 && t < p.g;
+    uint32_t off = 0;
+    uint64_t k = t + 1;  // boundary of the walk's current entry
+    if (lane < 4) rec[SYNC_WAVE + lane] = 0xff;
+    rec[lane] = 0xff;
+    __builtin_amdgcn_wave_barrier();
+    if (active) {
+      off = walk_segment(t, 0, lut, p);
+      rec[lane] = (uint8_t)off;
+    }
+    __builtin_amdgcn_wave_barrier();
+    while (__any(active)) {
+      if (active) {
+        if (k > kcap || k >= p.g) {
+          active = false;
+        } else {
+          const uint32_t e = walk_segment(k, off, lut, p);
+          ++k;
+          const uint32_t idx = (uint32_t)((int64_t)k - w0 - 1);
+          if (rec[idx] == e) {
+            active = false;
+          } else {
+            rec[idx] = (uint8_t)e;
+            off = e;
+          }
+        }
       }
-      uint32_t off = 0;
-      off = walk_word<false>(w[0], w[1], off, lut, p);
-      off = walk_word<false>(w[1], w[2], off, lut, p);
-      off = walk_word<false>(w[2], w[3], off, lut, p);
-      a = walk_word<true>(w[3], w[4], off, lut, p);
-      off = walk_word<false>(w[4], w[5], a, lut, p);
-      off = walk_word<false>(w[5], w[6], off, lut, p);
-      off = walk_word<false>(w[6], w[7], off, lut, p);
-      b = walk_word<true>(w[7], w[8], off, lut, p);
+      __builtin_amdgcn_wave_barrier();
+    }
+    const bool mine = lane >= halo && ts >= 0 && t < p.g;
+    uint32_t a = 0, b = 0;
+    if (mine) {
+      a = rec[lane];
+      b = rec[lane + 1];
       // no codeword crosses the end of the stream: the entry at 128g is 0, as the
       // encoder leaves the last gap (encoder.cu:414 memset, nothing crosses 128G)
       if (t + 1 >= p.g) a = 0;
       if (t + 2 >= p.g) b = 0;
     }
-    uint32_t v = a << (4 * (t & 7));
+    // w0 is a multiple of 8, so lane groups of 8 (4) are gap (pair) words
+    uint32_t v = a << (4 * (lane & 7));
     v |= __shfl_xor(v, 1);
     v |= __shfl_xor(v, 2);
     v |= __shfl_xor(v, 4);
-    if ((t & 7) == 0 && t < p.g) p.gaps[t >> 3] = v;
-    uint32_t q = (a | b << 4) << (8 * (t & 3));
+    if ((lane & 7) == 0 && mine) p.gaps[t >> 3] = v;
+    uint32_t q = (a | b << 4) << (8 * (lane & 3));
     q |= __shfl_xor(q, 1);
     q |= __shfl_xor(q, 2);
-    if ((t & 3) == 0 && t < p.g) p.pairs[t >> 2] = q;
+    if ((lane & 3) == 0 && mine) p.pairs[t >> 2] = q;
+    __builtin_amdgcn_wave_barrier();  // rec is reused by the wave's next segments
   }
 }
 
@@ -174,15 +237,7 @@ __device__ __forceinline__ void pair_store(uint32_t* pairs, uint64_t i, uint32_t
 // replaced together by one CAS, so a pass never sees a torn pair.
 __device__ void repair_chain(uint64_t j, uint32_t a, const uint16_t* lut, const SyncParams& p) {
   for (uint32_t s = 0; s < SYNC_CHAIN; ++s) {
-    const uint64_t w0 = 4 * (j + 1);
-    uint32_t w[5];
-#pragma unroll
-    for (int i = 0; i < 5; ++i) w[i] = ld_word(p.words, p.w, w0 + i);
-    uint32_t off = a;
-    off = walk_word<false>(w[0], w[1], off, lut, p);
-    off = walk_word<false>(w[1], w[2], off, lut, p);
-    off = walk_word<false>(w[2], w[3], off, lut, p);
-    uint32_t b = walk_word<true>(w[3], w[4], off, lut, p);
+    uint32_t b = walk_segment(j + 1, a, lut, p);
     if (j + 2 >= p.g) b = 0;
     pair_store(p.pairs, j, a | b << 4);
     if (j + 2 >= p.g) break;
@@ -304,6 +359,11 @@ extern "C" int gh_sync_gaps(int device, const gh_sym* syms, uint32_t nsyms, cons
   p.gaps = d_gap_words;
   p.pairs = (uint32_t*)pairs.p;
   p.counter = (unsigned int*)counter.p;
+  {
+    const char* eh = getenv("GH_SYNC_HALO");
+    const int h = eh ? atoi(eh) : SYNC_HALO;
+    p.halo = (uint32_t)std::clamp(h - h % 8, 0, 56);
+  }
   hipEvent_t e0, e1;
   GH_HIPS(hipEventCreate(&e0));
   GH_HIPS(hipEventCreate(&e1));
@@ -311,7 +371,7 @@ extern "C" int gh_sync_gaps(int device, const gh_sym* syms, uint32_t nsyms, cons
     hipEvent_t a, b;
     ~EvGuard() { (void)hipEventDestroy(a); (void)hipEventDestroy(b); }
   } evg{e0, e1};
-  const int gs = grid_for((const void*)gh_sync_kernel, g);
+  const int gs = grid_for((const void*)gh_sync_kernel, ceil_div(g, SYNC_WAVE - p.halo) * SYNC_WAVE);
   const int gf = grid_for((const void*)gh_sync_fix_kernel, g);
   GH_HIPS(hipMemsetAsync(counter.p, 0, 4, st));
   GH_HIPS(hipEventRecord(e0, st));
@@ -323,11 +383,11 @@ extern "C" int gh_sync_gaps(int device, const gh_sym* syms, uint32_t nsyms, cons
   for (;;) {
     hipLaunchKernelGGL(gh_sync_fix_kernel, dim3(gf), dim3(SYNC_TB), 0, st, p);
     GH_HIPS(hipGetLastError());
-    if (passes == 0) GH_HIPS(hipEventRecord(e1, st));
+    GH_HIPS(hipEventRecord(e1, st));
     unsigned int cnt = 0;
     GH_HIPS(hipMemcpyAsync(&cnt, counter.p, 4, hipMemcpyDeviceToHost, st));
     GH_HIPS(hipStreamSynchronize(st));
-    if (passes == 0) GH_HIPS(hipEventElapsedTime(&ms, e0, e1));
+    GH_HIPS(hipEventElapsedTime(&ms, e0, e1));
     ++passes;
     if (cnt == 0) break;
     mism += cnt;

@@ -213,7 +213,8 @@ typedef struct gh_sync_report {
   uint64_t g;           /* 128-bit segments = ceil(w / 4)                          */
   uint64_t mismatches;  /* segment boundaries the first walk got wrong (repaired)  */
   uint32_t passes;      /* verify/repair passes (1 when the first walk was right)  */
-  float kernel_ms;      /* sync walk + first verify pass, HIP events               */
+  float kernel_ms;      /* walk kernel to the last verify pass (HIP events; includes
+                           the host turnaround between passes)                     */
 } gh_sync_report;
 /* Gap words (ceil(ceil(w/4)/8) u32, the gap-array file's layout) of the raw stream
  * d_words[0..w) (device memory, 16-byte aligned) into d_gap_words on `hip_stream`

@@ -215,3 +215,16 @@ def test_gpu_decode_raw_large_property(gpu, orc):
     import ctypes
     pw = np.ctypeslib.as_array(ctypes.cast(s.c.payload, ctypes.POINTER(ctypes.c_uint32)), (s.w,))
     assert np.array_equal(gpu.decode_raw(pw.copy(), s.symbols, d.size), d)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("halo", ["0", "8", "56"])
+def test_gpu_sync_halo_variants(gpu, orc, halo, monkeypatch):
+    """Warm-up lanes per wave (GH_SYNC_HALO) change only how much the verify pass has to
+    repair, never the gaps."""
+    monkeypatch.setenv("GH_SYNC_HALO", halo)
+    d = orc.generate(9, 0.5, 400_009)
+    syms = orc.symbols_of(d)
+    units = orc.raw_encode(d, syms)
+    gaps, rep = _sync_on_gpu(gpu, units, syms)
+    assert np.array_equal(gaps, orc.raw_gaps(d, syms))
