@@ -47,6 +47,7 @@ EXPORTED = (
     "gh_device_count", "gh_version", "gh_last_error",
     "gh_ectx_create", "gh_ectx_destroy", "gh_ectx_load", "gh_ectx_plan", "gh_ectx_encode",
     "gh_ectx_download", "gh_ctx_device", "gh_sync_gaps", "gh_ctx_load_raw",
+    "gh_ctx_load_file", "gh_ctx_save_file",
 )
 
 
@@ -85,6 +86,12 @@ class gh_report(ctypes.Structure):
         ("mode", ctypes.c_uint32), ("path", ctypes.c_uint32),
         ("slow_lookbacks", ctypes.c_uint64),
     ]
+
+
+class gh_file_info(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint64), ("w", ctypes.c_uint64), ("g", ctypes.c_uint64),
+                ("nsyms", ctypes.c_uint32), ("version", ctypes.c_uint32), ("bytes_read", ctypes.c_uint64),
+                ("setup_ms", ctypes.c_double), ("transfer_ms", ctypes.c_double), ("total_ms", ctypes.c_double)]
 
 
 class gh_sync_report(ctypes.Structure):
@@ -142,6 +149,8 @@ def lib() -> ctypes.CDLL:
             "gh_ctx_device": ([P, ctypes.POINTER(I)], I),
             "gh_sync_gaps": ([I, P, U32, P, U64, P, P, ctypes.POINTER(gh_sync_report)], I),
             "gh_ctx_load_raw": ([P, P, U32, U64, P, U64, U64, ctypes.POINTER(gh_sync_report)], I),
+            "gh_ctx_load_file": ([P, ctypes.c_char_p, U64, U64, U64, ctypes.POINTER(gh_file_info)], I),
+            "gh_ctx_save_file": ([P, ctypes.c_char_p, U64, U64, U64, I, ctypes.POINTER(ctypes.c_double)], I),
             "gh_version": ([], ctypes.c_char_p),
             "gh_last_error": ([], ctypes.c_char_p),
         }
@@ -339,6 +348,25 @@ class Decoder:
         seg_end = stream.g if seg_end is None else seg_end
         self._stream = stream
         _check(lib().gh_ctx_load(self._h, ctypes.byref(stream.c), seg_begin, seg_end, out_cap))
+
+    def load_file(self, path: str, seg_begin: int = 0, seg_end: Optional[int] = None,
+                  out_cap: int = 0) -> gh_file_info:
+        """Stream segments [seg_begin, seg_end) of a compressed.huff file to the device
+        (pinned double-buffered read -> H2D); returns the header sizes and timings."""
+        info = gh_file_info()
+        _check(lib().gh_ctx_load_file(self._h, os.fsencode(path), seg_begin,
+                                      (1 << 64) - 1 if seg_end is None else seg_end, out_cap,
+                                      ctypes.byref(info)))
+        self._stream = None
+        return info
+
+    def save_file(self, path: str, nbytes: int, file_offset: int = 0, offset: int = 0,
+                  truncate: bool = True) -> float:
+        """Write decoded bytes [offset, offset+nbytes) to `path` at file_offset; wall ms."""
+        ms = ctypes.c_double()
+        _check(lib().gh_ctx_save_file(self._h, os.fsencode(path), file_offset, offset, nbytes,
+                                      int(truncate), ctypes.byref(ms)))
+        return ms.value
 
     def load_raw(self, symbols: Sequence[tuple], n: int, units, out_cap: int = 0) -> gh_sync_report:
         """Load a raw (gap-less) stream: u32 ``units``, canonical ``symbols`` list

@@ -49,48 +49,56 @@ int main(int argc, char** argv) {
   if (ngpus < 1) ngpus = 1;
   if (reps < 1) reps = 1;
 
-  FILE* f = std::fopen(argv[1], "rb");
-  if (!f) {
-    std::fprintf(stderr, "decoder: Could not open input file %s\n", argv[1]);
-    return 1;
-  }
-  std::fseek(f, 0, SEEK_END);
-  const long flen = std::ftell(f);
-  std::fseek(f, 0, SEEK_SET);
-  std::vector<uint8_t> file((size_t)std::max(flen, 0L));
-  if (flen > 0 && std::fread(file.data(), 1, (size_t)flen, f) != (size_t)flen) {
+  // Header first (sizes for the shard plan); each shard then streams its own payload
+  // range from the file (gh_ctx_load_file: pinned double-buffered read -> H2D).
+  gh_stream s{};
+  {
+    FILE* f = std::fopen(argv[1], "rb");
+    if (!f) {
+      std::fprintf(stderr, "decoder: Could not open input file %s\n", argv[1]);
+      return 1;
+    }
     std::fclose(f);
-    std::fprintf(stderr, "decoder: File read error\n");
-    return 1;
   }
-  std::fclose(f);
-
-  gh_stream s;
-  int rc = gh_stream_parse(file.data(), file.size(), &s);
-  if (rc) return die("bad compressed stream", rc);
-
-  std::printf("Input file: %s\n", argv[1]);
-  std::printf("Original size: %llu bytes\n", (unsigned long long)s.n);
-  std::printf("Compressed size: %llu bytes\n", (unsigned long long)s.w);  // reference prints W
-
   const int ndev = gh_device_count();
   if (ndev < 1) return die("no HIP device", GH_E_NODEV);
   if (ngpus > ndev) ngpus = ndev;
-
-  std::vector<uint64_t> bounds(ngpus + 1);
-  gh_plan_shards(s.g, (uint32_t)ngpus, bounds.data());
   std::vector<gh_ctx*> ctx(ngpus, nullptr);
   auto cleanup = [&]() {
     for (auto* c : ctx) gh_ctx_destroy(c);
   };
+  int rc;
   const double t0 = now_ms();
-  for (int k = 0; k < ngpus; ++k) {
-    if ((rc = gh_ctx_create(k, &ctx[k]))) { cleanup(); return die("device init", rc); }
-    if ((rc = gh_ctx_load(ctx[k], &s, bounds[k], bounds[k + 1], ngpus == 1 ? s.n : 0))) {
+  gh_file_info info{};
+  if ((rc = gh_ctx_create(0, &ctx[0]))) { cleanup(); return die("device init", rc); }
+  std::vector<uint64_t> bounds(ngpus + 1, 0);
+  if (ngpus == 1) {
+    if ((rc = gh_ctx_load_file(ctx[0], argv[1], 0, UINT64_MAX, 0, &info))) {
       cleanup();
-      return die("upload", rc);
+      return die("bad compressed stream / upload", rc);
+    }
+    bounds[1] = info.g;
+  } else {
+    // a zero-segment load reads just the header
+    if ((rc = gh_ctx_load_file(ctx[0], argv[1], 0, 0, 0, &info))) {
+      cleanup();
+      return die("bad compressed stream / upload", rc);
+    }
+    gh_plan_shards(info.g, (uint32_t)ngpus, bounds.data());
+    for (int k = 0; k < ngpus; ++k) {
+      if (k && (rc = gh_ctx_create(k, &ctx[k]))) { cleanup(); return die("device init", rc); }
+      if ((rc = gh_ctx_load_file(ctx[k], argv[1], bounds[k], bounds[k + 1], 0, nullptr))) {
+        cleanup();
+        return die("upload", rc);
+      }
     }
   }
+  s.n = info.n;
+  s.w = info.w;
+  s.g = info.g;
+  std::printf("Input file: %s\n", argv[1]);
+  std::printf("Original size: %llu bytes\n", (unsigned long long)s.n);
+  std::printf("Compressed size: %llu bytes\n", (unsigned long long)s.w);  // reference prints W
   const double t1 = now_ms();
   for (int r = 0; r < reps; ++r)
     for (int k = 0; k < ngpus; ++k)
@@ -98,67 +106,70 @@ int main(int argc, char** argv) {
   std::vector<gh_report> rep(ngpus);
   float dec_ms = 0;
   uint32_t status = 0;
+  uint64_t total = 0;
   for (int k = 0; k < ngpus; ++k) {
     if ((rc = gh_ctx_report(ctx[k], nullptr, &rep[k]))) { cleanup(); return die("decode", rc); }
     dec_ms = std::max(dec_ms, rep[k].kernel_ms);
     status |= rep[k].status;
+    total += rep[k].symbols;
   }
+  if (status) {
+    cleanup();
+    std::fprintf(stderr, "decoder: device reported status 0x%x (corrupted stream?)\n", status);
+    return 1;
+  }
+  if (total < s.n) {
+    cleanup();
+    std::fprintf(stderr, "decoder: stream decoded to %llu < N symbols\n", (unsigned long long)total);
+    return 1;
+  }
+  // each shard writes its bytes at its offset of argv[2] (pinned double-buffered
+  // D2H -> pwrite); the reference always wrote "decodedfile" (huff.cpp:32)
   const double t2 = now_ms();
-  std::vector<uint8_t> out((size_t)s.n + 16);
   uint64_t off = 0;
   for (int k = 0; k < ngpus; ++k) {
     const uint64_t want = off < s.n ? std::min<uint64_t>(rep[k].symbols, s.n - off) : 0;
-    if (want && (rc = gh_ctx_download(ctx[k], 0, out.data() + off, want))) {
+    if ((rc = gh_ctx_save_file(ctx[k], argv[2], off, 0, want, k == 0, nullptr))) {
       cleanup();
-      return die("download", rc);
+      return die("write output", rc);
     }
     off += rep[k].symbols;
   }
   const double t3 = now_ms();
   cleanup();
-  if (status) {
-    std::fprintf(stderr, "decoder: device reported status 0x%x (corrupted stream?)\n", status);
-    return 1;
-  }
-  if (off < s.n) {
-    std::fprintf(stderr, "decoder: stream decoded to %llu < N symbols\n", (unsigned long long)off);
-    return 1;
-  }
   std::printf("HtoD,%f, dec,%f, DtoH,%f,SEGMENTSIZE,%d,THREAD_NUM,%d,LOCAL_SEGMENT_NUM,%d\n",
               t1 - t0, dec_ms, t3 - t2, GH_SEGMENT_BITS, 256, 1);
   const double total_ms = (t1 - t0) + dec_ms + (t3 - t2);
   std::printf("Decode time: %.3f ms\n", total_ms);
   std::printf("Throughput: %.2f MB/s\n", (double)s.n / (1024.0 * 1024.0) / (total_ms / 1000.0));
 
-  FILE* o = std::fopen(argv[2], "wb");
-  if (!o) {
-    std::fprintf(stderr, "decoder: Could not open output file %s\n", argv[2]);
-    return 1;
-  }
-  if (s.n && std::fwrite(out.data(), 1, (size_t)s.n, o) != (size_t)s.n) {
-    std::fclose(o);
-    std::fprintf(stderr, "decoder: write error\n");
-    return 1;
-  }
-  std::fclose(o);
-
   int ok = -1;
   if (verify) {
+    // compare the written file with the reference bytes, chunk by chunk
     FILE* v = std::fopen(verify, "rb");
+    FILE* o = std::fopen(argv[2], "rb");
     ok = 0;
-    if (v) {
-      std::vector<uint8_t> ref((size_t)s.n + 1);
-      const size_t got = std::fread(ref.data(), 1, (size_t)s.n + 1, v);
-      std::fclose(v);
-      ok = (got == s.n && std::memcmp(ref.data(), out.data(), (size_t)s.n) == 0) ? 1 : 0;
+    if (v && o) {
+      std::vector<uint8_t> x(1 << 24), y(1 << 24);
+      ok = 1;
+      uint64_t seen = 0;
+      for (;;) {
+        const size_t a = std::fread(x.data(), 1, x.size(), v), b = std::fread(y.data(), 1, y.size(), o);
+        if (a != b || std::memcmp(x.data(), y.data(), a)) { ok = 0; break; }
+        seen += a;
+        if (a == 0) break;
+      }
+      if (seen != s.n) ok = 0;
     }
+    if (v) std::fclose(v);
+    if (o) std::fclose(o);
     std::printf("Verification: %s\n", ok ? "PASS" : "FAIL");
   }
   if (json) {
     const double kbytes = 4.0 * s.w + 4.0 * ((s.g + 7) / 8) + (double)s.n;
     std::printf(
         "{\"N\": %llu, \"W\": %llu, \"G\": %llu, \"gpus\": %d, \"reps\": %d, \"kernel_ms\": %.6f, "
-        "\"h2d_ms\": %.3f, \"d2h_ms\": %.3f, \"decoded_GBps\": %.3f, \"alg_bytes\": %.0f, "
+        "\"load_ms\": %.3f, \"save_ms\": %.3f, \"decoded_GBps\": %.3f, \"alg_bytes\": %.0f, "
         "\"alg_GBps\": %.3f, \"lut_bits\": %u, \"bitexact\": %s}\n",
         (unsigned long long)s.n, (unsigned long long)s.w, (unsigned long long)s.g, ngpus, reps,
         dec_ms, t1 - t0, t3 - t2, dec_ms > 0 ? s.n / (dec_ms * 1e6) : 0.0, kbytes,

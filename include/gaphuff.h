@@ -200,6 +200,30 @@ int gh_ctx_reset_timing(gh_ctx* ctx);
 /* HIP device ordinal the context is bound to. */
 int gh_ctx_device(gh_ctx* ctx, int* device);
 
+/* ---- streaming file I/O ------------------------------ */
+/* Replaces the reference CLI's whole-file fread + synchronous copies
+ * (decoder/src/huff.cpp:90-140, decoder.cu:759-768): the file's gap words and the
+ * shard's payload words stream through two pinned buffers, the read of one chunk
+ * overlapping the H2D of the previous one. */
+typedef struct gh_file_info {
+  uint64_t n, w, g;        /* stream sizes from the header                          */
+  uint32_t nsyms, version;
+  uint64_t bytes_read;     /* header + gap words + the shard's payload words        */
+  double setup_ms;         /* open, header parse, allocations (wall)                */
+  double transfer_ms;      /* overlapped file reads + H2D (wall)                    */
+  double total_ms;         /* whole call (wall), including table build              */
+} gh_file_info;
+/* gh_ctx_load for segments [seg_begin, seg_end) of the compressed.huff at `path`
+ * (seg_end = UINT64_MAX: to the end).  info may be NULL. */
+int gh_ctx_load_file(gh_ctx* ctx, const char* path, uint64_t seg_begin, uint64_t seg_end,
+                     uint64_t out_cap, gh_file_info* info);
+/* Wait for the context's decode, then write output bytes [byte_offset,
+ * byte_offset+nbytes) to `path` at file_offset (pwrite; the file is created, and
+ * truncated first when `truncate`), the D2H of one chunk overlapping the write of the
+ * previous one.  ms (may be NULL): wall time. */
+int gh_ctx_save_file(gh_ctx* ctx, const char* path, uint64_t file_offset, uint64_t byte_offset,
+                     uint64_t nbytes, int truncate, double* ms);
+
 /* ---- self-synchronising decode of gap-less streams ---- */
 /* Replaces CUHD's decoder for raw Huffman streams without a gap array
  * (gpuhd/src/cuhd_gpu_decoder.cu:145-523, CUHDGPUDecoder::decode declared at

@@ -1,0 +1,85 @@
+"""Streaming file I/O: gh_ctx_load_file / gh_ctx_save_file and
+the decoder CLI built on them.  Decoded files must equal the input bytes (the oracle
+and the reference sequential.cpp pin the stream format, tests/test_oracle.py)."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "bin")
+
+
+def _write(tmp_path, gh, seed, r, n, name="c.huff"):
+    d = gh.generate(seed, r, n)
+    p = tmp_path / name
+    gh.encode(d, threads=8).tofile(p)
+    return d, str(p)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("r,n", [(0.5, 1), (0.5, 3_000_017), (0.1, 80_000_000)])
+def test_gpu_load_save_file_roundtrip(gpu, tmp_path, r, n):
+    """80 MB at r=0.1 streams in three 32 MiB chunks each way."""
+    d, path = _write(tmp_path, gpu, 3, r, n)
+    out = str(tmp_path / "out.bin")
+    with gpu.Decoder(0) as dec:
+        info = dec.load_file(path)
+        assert info.n == n and info.bytes_read == os.path.getsize(path)
+        dec.decode()
+        assert dec.report().status == 0
+        dec.save_file(out, n)
+    assert np.array_equal(np.fromfile(out, dtype=np.uint8), d)
+
+
+@pytest.mark.gpu
+def test_gpu_load_file_shards(gpu, tmp_path):
+    """Three shards, each loading only its payload range and writing at its offset."""
+    d, path = _write(tmp_path, gpu, 4, 0.9, 5_000_000)
+    out = str(tmp_path / "out.bin")
+    g = gpu.parse(np.fromfile(path, dtype=np.uint8)).g
+    b = gpu.plan_shards(g, 3)
+    off = 0
+    for k in range(3):
+        with gpu.Decoder(0) as dec:
+            info = dec.load_file(path, b[k], b[k + 1])
+            dec.decode()
+            sym = dec.report().symbols
+            want = min(sym, d.size - off)
+            dec.save_file(out, want, file_offset=off, truncate=(k == 0))
+            off += sym
+            assert info.bytes_read < os.path.getsize(path) or k == 2
+    assert np.array_equal(np.fromfile(out, dtype=np.uint8), d)
+
+
+@pytest.mark.gpu
+def test_gpu_load_file_empty_and_truncated(gpu, tmp_path):
+    d, path = _write(tmp_path, gpu, 5, 0.5, 0)
+    with gpu.Decoder(0) as dec:
+        info = dec.load_file(path)
+        assert info.n == 0
+        dec.decode()
+        dec.save_file(str(tmp_path / "e.bin"), 0)
+    assert os.path.getsize(tmp_path / "e.bin") == 0
+    _, path = _write(tmp_path, gpu, 5, 0.5, 100_000, "t.huff")
+    raw = open(path, "rb").read()
+    open(path, "wb").write(raw[: len(raw) // 2])
+    with gpu.Decoder(0) as dec:
+        with pytest.raises(gpu.GapHuffError):
+            dec.load_file(path)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gpus", [1, 2])
+def test_gpu_cli_streaming_verify(gpu, tmp_path, gpus):
+    if not os.access(os.path.join(BIN, "decoder"), os.X_OK):
+        pytest.fail("bin/decoder not built")
+    d, path = _write(tmp_path, gpu, 6, 0.1, 40_000_003)
+    (tmp_path / "orig.bin").write_bytes(d.tobytes())
+    out = str(tmp_path / "dec.bin")
+    r = subprocess.run([os.path.join(BIN, "decoder"), path, out, "--gpus", str(gpus), "--verify",
+                        str(tmp_path / "orig.bin")], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "Verification: PASS" in r.stdout
+    assert np.array_equal(np.fromfile(out, dtype=np.uint8), d)
