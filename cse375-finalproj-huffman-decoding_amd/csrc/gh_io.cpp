@@ -172,7 +172,7 @@ extern "C" int gh_ctx_load_file(gh_ctx* ctx, const char* path, uint64_t seg_begi
     info->g = s.g;
     info->nsyms = s.nsyms;
     info->version = s.version;
-    info->bytes_read = hn + 4 * gw + 4 * (w1 - w0);
+    info->bytes_read = gap_off + 4 * gw + 4 * (w1 - w0);
     info->setup_ms = t1 - t0;
     info->transfer_ms = t2 - t1;
     info->total_ms = now_ms() - t0;
