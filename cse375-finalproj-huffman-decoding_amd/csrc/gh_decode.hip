@@ -2714,7 +2714,7 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
   GH_HIP(hipMemset(c->d_gran, 0, 8ull * c->gran_words));
   // start bit of local segment 0, and the gap nibble base for the rest
   c->first_start = 0;
-  if (b > 0) {
+  if (b > 0 && s->gap_words) {  // (gh_ctx_load_device reads it from device memory)
     const uint64_t nib = b - 1;
     uint32_t wv;
     std::memcpy(&wv, (const uint8_t*)s->gap_words + 4 * (nib >> 3), 4);

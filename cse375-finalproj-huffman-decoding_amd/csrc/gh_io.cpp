@@ -15,7 +15,11 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <map>
+#include <mutex>
+#include <thread>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -47,25 +51,58 @@ struct Fd {
   }
 };
 
-// Two pinned buffers, a stream and one event per buffer.
+// Two pinned buffers, a stream and one event per buffer, per device.  Pinning 64 MiB
+// costs tens of milliseconds, so the buffers are kept for the life of the process and
+// handed to one call at a time.
 struct Staging {
   void* buf[2] = {nullptr, nullptr};
   hipEvent_t ev[2] = {nullptr, nullptr};
   hipStream_t st = nullptr;
-  ~Staging() {
-    for (int i = 0; i < 2; ++i) {
-      if (ev[i]) (void)hipEventDestroy(ev[i]);
-      if (buf[i]) (void)hipHostFree(buf[i]);
-    }
-    if (st) (void)hipStreamDestroy(st);
-  }
   int init() {
+    if (st) return GH_OK;
     GH_HIPI(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     for (int i = 0; i < 2; ++i) {
       GH_HIPI(hipHostMalloc(&buf[i], IO_CHUNK, hipHostMallocDefault));
       GH_HIPI(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
     }
     return GH_OK;
+  }
+};
+
+std::mutex g_pool_mu;
+std::map<int, Staging*> g_pool;  // device -> idle staging set (never freed)
+
+// Takes the device's staging set (or makes one) for the duration of a call.
+struct StagingLease {
+  int dev;
+  Staging* s = nullptr;
+  explicit StagingLease(int d) : dev(d) {}
+  int acquire() {
+    {
+      std::lock_guard<std::mutex> g(g_pool_mu);
+      auto it = g_pool.find(dev);
+      if (it != g_pool.end() && it->second) {
+        s = it->second;
+        it->second = nullptr;
+      }
+    }
+    if (!s) s = new Staging();
+    return s->init();
+  }
+  ~StagingLease() {
+    if (!s) return;
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    Staging*& slot = g_pool[dev];
+    if (!slot) {
+      slot = s;  // keep one set per device
+    } else {
+      for (int i = 0; i < 2; ++i) {
+        if (s->ev[i]) (void)hipEventDestroy(s->ev[i]);
+        if (s->buf[i]) (void)hipHostFree(s->buf[i]);
+      }
+      if (s->st) (void)hipStreamDestroy(s->st);
+      delete s;
+    }
   }
 };
 
@@ -93,13 +130,33 @@ bool write_full(int fd, const void* src, size_t n, uint64_t off) {
   return true;
 }
 
+// A chunk's reads split over IO_THREADS threads (one page-cache copy stream per
+// thread runs at a few GB/s).
+constexpr int IO_THREADS = 4;
+template <class F>
+bool par_io(size_t n, F f) {
+  if (n < (4u << 20)) return f(0, n);
+  std::atomic<bool> ok{true};
+  std::vector<std::thread> th;
+  const size_t part = ((n + IO_THREADS - 1) / IO_THREADS + 4095) & ~size_t(4095);
+  for (int i = 0; i < IO_THREADS; ++i) {
+    const size_t a = std::min(n, i * part), b = std::min(n, a + part);
+    if (a < b) th.emplace_back([&, a, b] { if (!f(a, b - a)) ok = false; });
+  }
+  for (auto& t : th) t.join();
+  return ok;
+}
+
 // File bytes [off, off+n) -> device dst, double-buffered.
 int stream_h2d(Staging& s, int fd, uint64_t off, uint64_t n, uint8_t* dst) {
   int b = 0;
   for (uint64_t done = 0; done < n; b ^= 1) {
     const size_t c = (size_t)std::min<uint64_t>(IO_CHUNK, n - done);
     GH_HIPI(hipEventSynchronize(s.ev[b]));  // the DMA that last used this buffer
-    if (!read_full(fd, s.buf[b], c, off + done)) return fail(GH_E_FORMAT, "short read of the stream file");
+    uint8_t* hb = (uint8_t*)s.buf[b];
+    const uint64_t base = off + done;
+    if (!par_io(c, [&](size_t a, size_t m) { return read_full(fd, hb + a, m, base + a); }))
+      return fail(GH_E_FORMAT, "short read of the stream file");
     GH_HIPI(hipMemcpyAsync(dst + done, s.buf[b], c, hipMemcpyHostToDevice, s.st));
     GH_HIPI(hipEventRecord(s.ev[b], s.st));
     done += c;
@@ -149,8 +206,9 @@ extern "C" int gh_ctx_load_file(gh_ctx* ctx, const char* path, uint64_t seg_begi
   DevMem dpay, dgap;
   GH_HIPI(hipMalloc(&dpay.p, 4 * (w1 - w0) + 64));
   GH_HIPI(hipMalloc(&dgap.p, 4 * gw + 64));
-  Staging stg;
-  if ((rc = stg.init())) return rc;
+  StagingLease lease(dev);
+  if ((rc = lease.acquire())) return rc;
+  Staging& stg = *lease.s;
   const double t1 = now_ms();
   if ((rc = stream_h2d(stg, f.fd, gap_off, 4 * gw, (uint8_t*)dgap.p))) return rc;
   if ((rc = stream_h2d(stg, f.fd, pay_off + 4 * w0, 4 * (w1 - w0), (uint8_t*)dpay.p))) return rc;
@@ -198,8 +256,9 @@ extern "C" int gh_ctx_save_file(gh_ctx* ctx, const char* path, uint64_t file_off
   // the decode was enqueued on the context's stream: wait for it
   gh_report rep;
   if ((rc = gh_ctx_report(ctx, nullptr, &rep))) return rc;
-  Staging stg;
-  if ((rc = stg.init())) return rc;
+  StagingLease lease(dev);
+  if ((rc = lease.acquire())) return rc;
+  Staging& stg = *lease.s;
   const uint8_t* src = (const uint8_t*)dout + byte_offset;
   // D2H of chunk c+1 overlaps the write of chunk c
   uint64_t pend_off = 0;
@@ -213,7 +272,12 @@ extern "C" int gh_ctx_save_file(gh_ctx* ctx, const char* path, uint64_t file_off
     }
     if (pend_b >= 0) {
       GH_HIPI(hipEventSynchronize(stg.ev[pend_b]));
-      if (!write_full(f.fd, stg.buf[pend_b], pend_n, file_offset + pend_off))
+      const uint8_t* hb = (const uint8_t*)stg.buf[pend_b];
+      const uint64_t base = file_offset + pend_off;
+      const int fd = f.fd;
+      // one writer: concurrent pwrites to one file serialise on its inode lock and
+      // measured slower than a single stream of 32 MiB writes
+      if (!write_full(fd, hb, pend_n, base))
         return fail(GH_E_ARG, std::string("write error on ") + path);
     }
     if (!c) break;
