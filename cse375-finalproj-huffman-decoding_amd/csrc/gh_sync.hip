@@ -436,3 +436,24 @@ extern "C" int gh_ctx_load_raw(gh_ctx* ctx, const gh_sym* syms, uint32_t nsyms, 
   s.g = g;
   return gh_ctx_load_device(ctx, &s, 0, g, (const uint32_t*)dw.p, w, (const uint32_t*)dg.p, out_cap);
 }
+
+// Device-memory helpers for C/FFI callers that have no HIP binding of their own (e.g.
+// ctypes): buffers for gh_sync_gaps / gh_ctx_load_device.
+extern "C" int gh_dev_alloc(int device, uint64_t bytes, void** out) {
+  if (!out) return fail(GH_E_ARG, "null argument");
+  *out = nullptr;
+  GH_HIPS(hipSetDevice(device));
+  GH_HIPS(hipMalloc(out, std::max<uint64_t>(bytes, 1)));
+  return GH_OK;
+}
+
+extern "C" int gh_dev_free(void* p) {
+  GH_HIPS(hipFree(p));
+  return GH_OK;
+}
+
+extern "C" int gh_dev_copy(void* dst, const void* src, uint64_t bytes) {
+  if (bytes && (!dst || !src)) return fail(GH_E_ARG, "null argument");
+  if (bytes) GH_HIPS(hipMemcpy(dst, src, bytes, hipMemcpyDefault));
+  return GH_OK;
+}

@@ -47,7 +47,7 @@ EXPORTED = (
     "gh_device_count", "gh_version", "gh_last_error",
     "gh_ectx_create", "gh_ectx_destroy", "gh_ectx_load", "gh_ectx_plan", "gh_ectx_encode",
     "gh_ectx_download", "gh_ctx_device", "gh_sync_gaps", "gh_ctx_load_raw",
-    "gh_ctx_load_file", "gh_ctx_save_file",
+    "gh_ctx_load_file", "gh_ctx_save_file", "gh_dev_alloc", "gh_dev_free", "gh_dev_copy",
 )
 
 
@@ -151,6 +151,9 @@ def lib() -> ctypes.CDLL:
             "gh_ctx_load_raw": ([P, P, U32, U64, P, U64, U64, ctypes.POINTER(gh_sync_report)], I),
             "gh_ctx_load_file": ([P, ctypes.c_char_p, U64, U64, U64, ctypes.POINTER(gh_file_info)], I),
             "gh_ctx_save_file": ([P, ctypes.c_char_p, U64, U64, U64, I, ctypes.POINTER(ctypes.c_double)], I),
+            "gh_dev_alloc": ([I, U64, ctypes.POINTER(P)], I),
+            "gh_dev_free": ([P], I),
+            "gh_dev_copy": ([P, P, U64], I),
             "gh_version": ([], ctypes.c_char_p),
             "gh_last_error": ([], ctypes.c_char_p),
         }
@@ -429,6 +432,47 @@ def _syms(symbols: Sequence[tuple]):
     for i, (sy, ln) in enumerate(symbols):
         arr[i].symbol, arr[i].length = sy, ln
     return arr
+
+
+class DeviceBuffer:
+    """Device memory through the library's own HIP runtime (gh_dev_*)."""
+
+    def __init__(self, nbytes: int, device: int = 0):
+        self.ptr = ctypes.c_void_p()
+        self.nbytes = nbytes
+        _check(lib().gh_dev_alloc(device, nbytes, ctypes.byref(self.ptr)))
+
+    @property
+    def addr(self) -> int:
+        return int(self.ptr.value or 0)
+
+    def upload(self, a: np.ndarray) -> "DeviceBuffer":
+        a = np.ascontiguousarray(a)
+        assert a.nbytes <= self.nbytes
+        _check(lib().gh_dev_copy(self.ptr, _ptr(a), a.nbytes))
+        return self
+
+    def download(self, a: np.ndarray) -> np.ndarray:
+        assert a.flags.c_contiguous and a.nbytes <= self.nbytes
+        _check(lib().gh_dev_copy(_ptr(a), self.ptr, a.nbytes))
+        return a
+
+    def close(self) -> None:
+        if self.ptr:
+            lib().gh_dev_free(self.ptr)
+            self.ptr = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def sync_gaps(symbols: Sequence[tuple], d_words: int, w: int, d_gap_words: int, device: int = 0,

@@ -268,6 +268,12 @@ int gh_decode(const gh_stream* s, uint8_t* out, uint64_t out_len, const gh_opts*
 /* Evenly split G segments into `nshards` contiguous ranges: bounds[0..nshards]. */
 int gh_plan_shards(uint64_t g, uint32_t nshards, uint64_t* bounds);
 
+/* Device memory for FFI callers without a HIP binding (buffers for gh_sync_gaps /
+ * gh_ctx_load_device).  gh_dev_copy: any direction (unified addressing). */
+int gh_dev_alloc(int device, uint64_t bytes, void** out);
+int gh_dev_free(void* p);
+int gh_dev_copy(void* dst, const void* src, uint64_t bytes);
+
 /* Number of visible HIP devices (0 when none / no driver). */
 int gh_device_count(void);
 /* Library version string. */

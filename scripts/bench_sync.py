@@ -17,12 +17,6 @@ import gaphuff as gh  # noqa: E402
 WORKLOADS = {"cfg2": (10**8, 0.5), "cfg3": (10**9, 0.9), "cfg4": (10**9, 0.1)}
 PEAK = 8000.0  # GB/s, MI355X HBM3E
 
-H = ctypes.CDLL("/opt/rocm/lib/libamdhip64.so")  # the runtime libgaphuff links
-H.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
-H.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
-H.hipFree.argtypes = [ctypes.c_void_p]
-
-
 def arr(ptr, n):
     return np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ctypes.c_uint32)), (max(n, 1),))[:n]
 
@@ -35,18 +29,13 @@ for wl in sys.argv[1:] or ["cfg2", "cfg3", "cfg4"]:
     payload = arr(s.c.payload, s.w).copy()
     gw = (s.g + 7) // 8
     want_gaps = arr(s.c.gap_words, gw).copy()
-    dw, dg = ctypes.c_void_p(), ctypes.c_void_p()
-    assert H.hipMalloc(ctypes.byref(dw), 4 * (s.w + 16)) == 0
-    assert H.hipMalloc(ctypes.byref(dg), 4 * (gw + 4)) == 0
-    assert H.hipMemcpy(dw, payload.ctypes.data, 4 * s.w, 1) == 0
-    for _ in range(3):
-        gh.sync_gaps(syms, dw.value, s.w, dg.value)
-    reps = [gh.sync_gaps(syms, dw.value, s.w, dg.value) for _ in range(10)]
-    sync_ms = float(np.median([x.kernel_ms for x in reps]))
-    got = np.empty(gw, np.uint32)
-    assert H.hipMemcpy(got.ctypes.data, dg, 4 * gw, 2) == 0
-    H.hipFree(dw)
-    H.hipFree(dg)
+    with gh.DeviceBuffer(4 * (s.w + 16)) as dw, gh.DeviceBuffer(4 * (gw + 4)) as dg:
+        dw.upload(payload)
+        for _ in range(3):
+            gh.sync_gaps(syms, dw.addr, s.w, dg.addr)
+        reps = [gh.sync_gaps(syms, dw.addr, s.w, dg.addr) for _ in range(10)]
+        sync_ms = float(np.median([x.kernel_ms for x in reps]))
+        got = dg.download(np.empty(gw, np.uint32))
     with gh.Decoder(0) as d:
         rep0 = d.load_raw(syms, n, payload)
         for _ in range(3):

@@ -97,36 +97,17 @@ def test_sync_abi_exports(gh):
 
 
 # ------------------------------------------------------------------------- GPU
-def _hip():
-    """The HIP runtime libgaphuff itself links (torch bundles another one, and two
-    runtimes in one process do not share the device)."""
-    import ctypes
-    L = ctypes.CDLL("/opt/rocm/lib/libamdhip64.so")
-    L.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
-    L.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
-    L.hipFree.argtypes = [ctypes.c_void_p]
-    return L
-
-
 def _sync_on_gpu(gh, units, syms):
-    import ctypes
-    H = _hip()
     w = int(units.size)
     g = (w + 3) // 4
     nw = (g + 7) // 8
     src = np.concatenate([units, np.zeros(4, np.uint32)]).astype(np.uint32)
     gaps = np.full(nw + 4, 0xFFFFFFFF, dtype=np.uint32)
-    dw, dg = ctypes.c_void_p(), ctypes.c_void_p()
-    assert H.hipMalloc(ctypes.byref(dw), src.nbytes) == 0
-    assert H.hipMalloc(ctypes.byref(dg), gaps.nbytes) == 0
-    try:
-        assert H.hipMemcpy(dw, src.ctypes.data, src.nbytes, 1) == 0  # H2D
-        assert H.hipMemcpy(dg, gaps.ctypes.data, gaps.nbytes, 1) == 0
-        rep = gh.sync_gaps(syms, dw.value, w, dg.value, device=0)
-        assert H.hipMemcpy(gaps.ctypes.data, dg, gaps.nbytes, 2) == 0  # D2H
-    finally:
-        H.hipFree(dw)
-        H.hipFree(dg)
+    with gh.DeviceBuffer(src.nbytes) as dw, gh.DeviceBuffer(gaps.nbytes) as dg:
+        dw.upload(src)
+        dg.upload(gaps)
+        rep = gh.sync_gaps(syms, dw.addr, w, dg.addr, device=0)
+        dg.download(gaps)
     assert np.all(gaps[nw:] == 0xFFFFFFFF), "wrote past the gap words"
     return gaps[:nw], rep
 
