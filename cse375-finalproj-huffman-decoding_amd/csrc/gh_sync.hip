@@ -55,7 +55,7 @@ namespace {
 constexpr int SK = 12;          // LUT prefix bits
 constexpr int SYNC_TB = 256;    // threads per workgroup
 constexpr uint32_t SYNC_CHAIN = 256;  // segments one repair chain may walk per pass
-constexpr int SYNC_HALO = 16;         // warm-up segments per wave (GH_SYNC_HALO overrides)
+constexpr int SYNC_HALO = 8;          // warm-up segments per wave (GH_SYNC_HALO overrides)
 
 #define GH_HIPS(expr)                                                             \
   do {                                                                            \

@@ -17,6 +17,7 @@ import gaphuff as gh  # noqa: E402
 WORKLOADS = {"cfg2": (10**8, 0.5), "cfg3": (10**9, 0.9), "cfg4": (10**9, 0.1)}
 PEAK = 8000.0  # GB/s, MI355X HBM3E
 
+
 def arr(ptr, n):
     return np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ctypes.c_uint32)), (max(n, 1),))[:n]
 
