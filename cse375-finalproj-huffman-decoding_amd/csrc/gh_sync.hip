@@ -92,7 +92,9 @@ __device__ __forceinline__ uint32_t long_len(uint32_t p16, const SyncParams& p) 
 // previous word's last codeword reached into this one) is the next start relative to
 // the top of `hi`; returns the first start at or after the next word, relative to it.
 // BOUND: the returned start is recorded, so no multi-codeword step may pass it.
-template <bool BOUND>
+// LONG: the code has codewords longer than SK bits (else every LUT entry has a length:
+// patterns outside the code space are stored as length 1, so no branch per step).
+template <bool BOUND, bool LONG>
 __device__ __forceinline__ uint32_t walk_word(uint32_t hi, uint32_t lo, uint32_t off,
                                               const uint16_t* lut, const SyncParams& p) {
   const uint64_t win = ((uint64_t)hi << 32) | lo;
@@ -101,7 +103,7 @@ __device__ __forceinline__ uint32_t walk_word(uint32_t hi, uint32_t lo, uint32_t
     const uint32_t e = lut[p16 >> (16 - SK)];
     const uint32_t adv = e >> 5;
     uint32_t len = e & 31u;
-    if (len == 0) len = long_len(p16, p);
+    if (LONG && len == 0) len = long_len(p16, p);
     off += (adv != 0 && (!BOUND || off + SK <= 32)) ? adv : len;
   }
   return off - 32;
@@ -115,10 +117,9 @@ __device__ __forceinline__ void stage_lut(uint16_t* lds, const uint16_t* g) {
 
 // Walk segment j (words 4j..4j+4) from entry offset `off`; returns the entry offset at
 // boundary 128(j+1).
-__device__ __forceinline__ uint32_t walk_segment(uint64_t j, uint32_t off, const uint16_t* lut,
-                                                 const SyncParams& p) {
+// Words 4j..4j+4 of segment j (zero past the stream).
+__device__ __forceinline__ void load_segment(uint64_t j, uint32_t (&w)[5], const SyncParams& p) {
   const uint64_t w0 = 4 * j;
-  uint32_t w[5];
   if (w0 + 5 <= p.w) {
     const uint4 x = *reinterpret_cast<const uint4*>(p.words + w0);
     w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w;
@@ -127,10 +128,27 @@ __device__ __forceinline__ uint32_t walk_segment(uint64_t j, uint32_t off, const
 #pragma unroll
     for (int i = 0; i < 5; ++i) w[i] = ld_word(p.words, p.w, w0 + i);
   }
-  off = walk_word<false>(w[0], w[1], off, lut, p);
-  off = walk_word<false>(w[1], w[2], off, lut, p);
-  off = walk_word<false>(w[2], w[3], off, lut, p);
-  return walk_word<true>(w[3], w[4], off, lut, p);
+}
+
+// Walk a segment's words from entry offset `off`; returns the entry offset at the
+// segment's end boundary.
+template <bool LONG>
+__device__ __forceinline__ uint32_t walk_words(const uint32_t (&w)[5], uint32_t off, const uint16_t* lut,
+                                               const SyncParams& p) {
+  off = walk_word<false, LONG>(w[0], w[1], off, lut, p);
+  off = walk_word<false, LONG>(w[1], w[2], off, lut, p);
+  off = walk_word<false, LONG>(w[2], w[3], off, lut, p);
+  return walk_word<true, LONG>(w[3], w[4], off, lut, p);
+}
+
+// Walk segment j from entry offset `off`; returns the entry offset at boundary
+// 128(j+1).
+template <bool LONG>
+__device__ __forceinline__ uint32_t walk_segment(uint64_t j, uint32_t off, const uint16_t* lut,
+                                                 const SyncParams& p) {
+  uint32_t w[5];
+  load_segment(j, w, p);
+  return walk_words<LONG>(w, off, lut, p);
 }
 
 // Each wavefront owns `out` = 64 - halo consecutive output segments [wo, wo+out); its
@@ -148,6 +166,7 @@ __device__ __forceinline__ uint32_t walk_segment(uint64_t j, uint32_t off, const
 // ordinary codes has long merged with the true path, so the verify pass rarely finds a
 // seam to repair.
 constexpr int SYNC_WAVE = 64;
+template <bool LONG>
 __global__ __launch_bounds__(SYNC_TB) void gh_sync_kernel(SyncParams p) {
   __shared__ uint16_t lut[1 << SK];
   __shared__ uint8_t rec_all[SYNC_TB / SYNC_WAVE][SYNC_WAVE + 4];
@@ -170,7 +189,7 @@ __global__ __launch_bounds__(SYNC_TB) void gh_sync_kernel(SyncParams p) {
     rec[lane] = 0xff;
     __builtin_amdgcn_wave_barrier();
     if (active) {
-      off = walk_segment(t, 0, lut, p);
+      off = walk_segment<LONG>(t, 0, lut, p);
       rec[lane] = (uint8_t)off;
     }
     __builtin_amdgcn_wave_barrier();
@@ -179,7 +198,7 @@ __global__ __launch_bounds__(SYNC_TB) void gh_sync_kernel(SyncParams p) {
         if (k > kcap || k >= p.g) {
           active = false;
         } else {
-          const uint32_t e = walk_segment(k, off, lut, p);
+          const uint32_t e = walk_segment<LONG>(k, off, lut, p);
           ++k;
           const uint32_t idx = (uint32_t)((int64_t)k - w0 - 1);
           if (rec[idx] == e) {
@@ -235,9 +254,10 @@ __device__ __forceinline__ void pair_store(uint32_t* pairs, uint64_t i, uint32_t
 // a_j := a (the entry at 128(j+1)); re-walk segment j+1 from it to get b_j, and keep
 // going while the new entry disagrees with the stored one.  (a, b) of one segment are
 // replaced together by one CAS, so a pass never sees a torn pair.
+template <bool LONG>
 __device__ void repair_chain(uint64_t j, uint32_t a, const uint16_t* lut, const SyncParams& p) {
   for (uint32_t s = 0; s < SYNC_CHAIN; ++s) {
-    uint32_t b = walk_segment(j + 1, a, lut, p);
+    uint32_t b = walk_segment<LONG>(j + 1, a, lut, p);
     if (j + 2 >= p.g) b = 0;
     pair_store(p.pairs, j, a | b << 4);
     if (j + 2 >= p.g) break;
@@ -247,6 +267,7 @@ __device__ void repair_chain(uint64_t j, uint32_t a, const uint16_t* lut, const 
   }
 }
 
+template <bool LONG>
 __global__ __launch_bounds__(SYNC_TB) void gh_sync_fix_kernel(SyncParams p) {
   __shared__ uint16_t lut[1 << SK];
   stage_lut(lut, p.lut);
@@ -256,7 +277,7 @@ __global__ __launch_bounds__(SYNC_TB) void gh_sync_fix_kernel(SyncParams p) {
     const uint32_t pt = pair_at(p.pairs, t), pn = pair_at(p.pairs, t + 1);
     if ((pt >> 4) != (pn & 15u)) {
       atomicAdd(p.counter, 1u);
-      repair_chain(t + 1, pt >> 4, lut, p);
+      repair_chain<LONG>(t + 1, pt >> 4, lut, p);
     }
   }
 }
@@ -303,6 +324,9 @@ void build_sync_tables(const Canon& c, SyncTables& st) {
       if (s == 0) first = l;
       s += l;
     }
+    // a prefix outside the code space (only met by walks that started mid-codeword)
+    // steps one bit, like long_len's fallback
+    if (first == 0 && (v << (16 - SK)) >= st.T[GH_MAX_CODE_LEN]) first = 1;
     st.lut[v] = (uint16_t)(first | (s << 5));
   }
 }
@@ -371,17 +395,21 @@ extern "C" int gh_sync_gaps(int device, const gh_sym* syms, uint32_t nsyms, cons
     hipEvent_t a, b;
     ~EvGuard() { (void)hipEventDestroy(a); (void)hipEventDestroy(b); }
   } evg{e0, e1};
-  const int gs = grid_for((const void*)gh_sync_kernel, ceil_div(g, SYNC_WAVE - p.halo) * SYNC_WAVE);
-  const int gf = grid_for((const void*)gh_sync_fix_kernel, g);
+  const bool lng = canon.maxlen > (uint32_t)SK;
+  const void* ks = lng ? (const void*)gh_sync_kernel<true> : (const void*)gh_sync_kernel<false>;
+  const void* kf = lng ? (const void*)gh_sync_fix_kernel<true> : (const void*)gh_sync_fix_kernel<false>;
+  const int gs = grid_for(ks, ceil_div(g, SYNC_WAVE - p.halo) * SYNC_WAVE);
+  const int gf = grid_for(kf, g);
+  void* kargs[] = {&p};
   GH_HIPS(hipMemsetAsync(counter.p, 0, 4, st));
   GH_HIPS(hipEventRecord(e0, st));
-  hipLaunchKernelGGL(gh_sync_kernel, dim3(gs), dim3(SYNC_TB), 0, st, p);
+  GH_HIPS(hipLaunchKernel(ks, dim3(gs), dim3(SYNC_TB), kargs, 0, st));
   GH_HIPS(hipGetLastError());
   uint64_t mism = 0;
   uint32_t passes = 0;
   float ms = 0;
   for (;;) {
-    hipLaunchKernelGGL(gh_sync_fix_kernel, dim3(gf), dim3(SYNC_TB), 0, st, p);
+    GH_HIPS(hipLaunchKernel(kf, dim3(gf), dim3(SYNC_TB), kargs, 0, st));
     GH_HIPS(hipGetLastError());
     GH_HIPS(hipEventRecord(e1, st));
     unsigned int cnt = 0;
