@@ -209,3 +209,35 @@ def test_gpu_sync_halo_variants(gpu, orc, halo, monkeypatch):
     units = orc.raw_encode(d, syms)
     gaps, rep = _sync_on_gpu(gpu, units, syms)
     assert np.array_equal(gaps, orc.raw_gaps(d, syms))
+
+
+def _random_code(rng, orc):
+    """A random canonical (symbol, length) list: package-merge lengths of random counts,
+    sometimes lengthened (incomplete code, Kraft < 1), lengths <= 16."""
+    ns = int(rng.integers(2, 257))
+    counts = np.sort(rng.geometric(rng.uniform(0.01, 0.5), ns).astype(np.uint64) *
+                     rng.integers(1, 1000, ns).astype(np.uint64))
+    lens = orc.package_merge(counts)  # ascending-count order
+    lens = sorted(lens)
+    if rng.random() < 0.5:  # make it incomplete
+        for i in range(len(lens) - 1, max(-1, len(lens) - 4), -1):
+            lens[i] = min(16, lens[i] + 1)
+        lens = sorted(lens)
+    syms = [int(x) for x in rng.permutation(256)[:ns]]
+    return list(zip(syms, lens))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(12))
+def test_gpu_sync_random_codes(gpu, orc, seed):
+    """Random codes (complete and incomplete, up to 16-bit codewords) and data drawn
+    with random skew: synthesised gaps equal the oracle's, the decode equals the data."""
+    rng = np.random.default_rng(1000 + seed)
+    syms = _random_code(rng, orc)
+    p = rng.dirichlet(np.full(len(syms), rng.uniform(0.05, 2.0)))
+    n = int(rng.integers(1, 200_000))
+    d = np.array([s for s, _ in syms], dtype=np.uint8)[rng.choice(len(syms), n, p=p)]
+    units = orc.raw_encode(d, syms)
+    gaps, _ = _sync_on_gpu(gpu, units, syms)
+    assert np.array_equal(gaps, orc.raw_gaps(d, syms))
+    assert np.array_equal(gpu.decode_raw(units, syms, n), d)
