@@ -289,3 +289,31 @@ extern "C" int gh_ctx_save_file(gh_ctx* ctx, const char* path, uint64_t file_off
   if (ms) *ms = now_ms() - t0;
   return GH_OK;
 }
+
+extern "C" int gh_raw_parse(const void* file, size_t len, gh_raw_stream* out) {
+  if (!file || !out) return fail(GH_E_ARG, "null argument");
+  const uint8_t* p = (const uint8_t*)file;
+  auto rd64 = [&](size_t o) {
+    uint64_t v;
+    std::memcpy(&v, p + o, 8);
+    return v;
+  };
+  if (len < 16 || rd64(0) != GH_RAW_MAGIC) return fail(GH_E_FORMAT, "not a raw-stream container");
+  const uint64_t ns = rd64(8);
+  if (ns > GH_MAX_SYMBOLS) return fail(GH_E_FORMAT, "symbol count > 256");
+  size_t off = 16 + 2 * ns;
+  if (len < off + 16) return fail(GH_E_FORMAT, "truncated raw-stream header");
+  gh_raw_stream r{};
+  r.syms = (const gh_sym*)(p + 16);
+  r.nsyms = (uint32_t)ns;
+  r.n = rd64(off);
+  r.w = rd64(off + 8);
+  off += 16;
+  if (r.w > (len - off) / 4) return fail(GH_E_FORMAT, "file shorter than its units");
+  r.units = (const uint32_t*)(p + off);
+  Canon c;
+  int rc = build_canon(r.syms, r.nsyms, c);
+  if (rc) return rc;
+  *out = r;
+  return GH_OK;
+}

@@ -48,6 +48,7 @@ EXPORTED = (
     "gh_ectx_create", "gh_ectx_destroy", "gh_ectx_load", "gh_ectx_plan", "gh_ectx_encode",
     "gh_ectx_download", "gh_ctx_device", "gh_sync_gaps", "gh_ctx_load_raw",
     "gh_ctx_load_file", "gh_ctx_save_file", "gh_dev_alloc", "gh_dev_free", "gh_dev_copy",
+    "gh_raw_parse",
 )
 
 
@@ -92,6 +93,11 @@ class gh_file_info(ctypes.Structure):
     _fields_ = [("n", ctypes.c_uint64), ("w", ctypes.c_uint64), ("g", ctypes.c_uint64),
                 ("nsyms", ctypes.c_uint32), ("version", ctypes.c_uint32), ("bytes_read", ctypes.c_uint64),
                 ("setup_ms", ctypes.c_double), ("transfer_ms", ctypes.c_double), ("total_ms", ctypes.c_double)]
+
+
+class gh_raw_stream(ctypes.Structure):
+    _fields_ = [("syms", ctypes.POINTER(gh_sym)), ("nsyms", ctypes.c_uint32), ("n", ctypes.c_uint64),
+                ("w", ctypes.c_uint64), ("units", ctypes.c_void_p)]
 
 
 class gh_sync_report(ctypes.Structure):
@@ -151,6 +157,7 @@ def lib() -> ctypes.CDLL:
             "gh_ctx_load_raw": ([P, P, U32, U64, P, U64, U64, ctypes.POINTER(gh_sync_report)], I),
             "gh_ctx_load_file": ([P, ctypes.c_char_p, U64, U64, U64, ctypes.POINTER(gh_file_info)], I),
             "gh_ctx_save_file": ([P, ctypes.c_char_p, U64, U64, U64, I, ctypes.POINTER(ctypes.c_double)], I),
+            "gh_raw_parse": ([P, ctypes.c_size_t, ctypes.POINTER(gh_raw_stream)], I),
             "gh_dev_alloc": ([I, U64, ctypes.POINTER(P)], I),
             "gh_dev_free": ([P], I),
             "gh_dev_copy": ([P, P, U64], I),
@@ -485,6 +492,17 @@ def sync_gaps(symbols: Sequence[tuple], d_words: int, w: int, d_gap_words: int, 
                               ctypes.c_void_p(d_gap_words), ctypes.c_void_p(hip_stream or None),
                               ctypes.byref(r)))
     return r
+
+
+def parse_raw(file_bytes):
+    """Parse a raw-stream container (bin/encoder --raw): (symbols, n, units)."""
+    raw = _u8(file_bytes)
+    r = gh_raw_stream()
+    _check(lib().gh_raw_parse(_ptr(raw), raw.size, ctypes.byref(r)))
+    syms = [(r.syms[i].symbol, r.syms[i].length) for i in range(r.nsyms)]
+    off = 16 + 2 * r.nsyms + 16
+    units = raw[off: off + 4 * r.w].view(np.uint32).copy()
+    return syms, int(r.n), units
 
 
 def decode_raw(units, symbols: Sequence[tuple], n: int, device: int = 0) -> np.ndarray:

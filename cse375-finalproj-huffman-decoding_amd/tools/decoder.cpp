@@ -1,4 +1,6 @@
-// bin/decoder <compressed.huff> <output> [--gpus N] [--reps R] [--json] [--verify FILE]
+// bin/decoder <compressed.huff | raw container> <output> [--gpus N] [--reps R] [--json] [--verify FILE]
+// A raw-stream container (bin/encoder --raw, GH_RAW_MAGIC) is decoded by the
+// self-synchronising path (gh_ctx_load_raw) on one GPU.
 //
 // Drop-in for the reference decoder CLI (Huffman_coding_Gap_arrays/decoder/src/
 // huff.cpp:22-142, used as `./bin/decoder in out` by run_huffman.sh:38), decoding on
@@ -52,14 +54,18 @@ int main(int argc, char** argv) {
   // Header first (sizes for the shard plan); each shard then streams its own payload
   // range from the file (gh_ctx_load_file: pinned double-buffered read -> H2D).
   gh_stream s{};
+  bool is_raw = false;  // gap-less raw-stream container (gh_ctx_load_raw, self-sync)
   {
     FILE* f = std::fopen(argv[1], "rb");
     if (!f) {
       std::fprintf(stderr, "decoder: Could not open input file %s\n", argv[1]);
       return 1;
     }
+    uint64_t magic = 0;
+    is_raw = std::fread(&magic, 1, 8, f) == 8 && magic == GH_RAW_MAGIC;
     std::fclose(f);
   }
+  if (is_raw) ngpus = 1;  // a raw stream's segment entries are found on one device
   const int ndev = gh_device_count();
   if (ndev < 1) return die("no HIP device", GH_E_NODEV);
   if (ngpus > ndev) ngpus = ndev;
@@ -72,7 +78,28 @@ int main(int argc, char** argv) {
   gh_file_info info{};
   if ((rc = gh_ctx_create(0, &ctx[0]))) { cleanup(); return die("device init", rc); }
   std::vector<uint64_t> bounds(ngpus + 1, 0);
-  if (ngpus == 1) {
+  if (is_raw) {
+    std::vector<uint8_t> file;
+    FILE* f = std::fopen(argv[1], "rb");
+    std::fseek(f, 0, SEEK_END);
+    file.resize((size_t)std::max(std::ftell(f), 0L));
+    std::fseek(f, 0, SEEK_SET);
+    const bool okr = std::fread(file.data(), 1, file.size(), f) == file.size();
+    std::fclose(f);
+    gh_raw_stream r;
+    gh_sync_report sr;
+    if (!okr || (rc = gh_raw_parse(file.data(), file.size(), &r)) ||
+        (rc = gh_ctx_load_raw(ctx[0], r.syms, r.nsyms, r.n, r.units, r.w, 0, &sr))) {
+      cleanup();
+      return die("bad raw stream / upload", okr ? rc : GH_E_FORMAT);
+    }
+    info.n = r.n;
+    info.w = r.w;
+    info.g = (r.w + 3) / 4;
+    bounds[1] = info.g;
+    std::printf("Raw stream: gap array built on the GPU in %.3f ms (%llu boundaries repaired)\n",
+                sr.kernel_ms, (unsigned long long)sr.mismatches);
+  } else if (ngpus == 1) {
     if ((rc = gh_ctx_load_file(ctx[0], argv[1], 0, UINT64_MAX, 0, &info))) {
       cleanup();
       return die("bad compressed stream / upload", rc);

@@ -1,4 +1,4 @@
-// bin/encoder <input> <compressed.huff> [--threads T] [--v2] [--gpu [DEVICE]]
+// bin/encoder <input> <compressed.huff> [--threads T] [--v2] [--gpu [DEVICE]] [--raw]
 //
 // Drop-in for the reference encoder CLI (Huffman_coding_Gap_arrays/encoder/src/
 // huff.cpp:30-220): same positional arguments, same output format (v1 header when
@@ -25,9 +25,11 @@ int main(int argc, char** argv) {
     return 1;
   }
   int threads = 0, force = 0, gpu = -1;
+  bool raw = false;  // write the gap-less raw-stream container (GH_RAW_MAGIC) instead
   for (int i = 3; i < argc; ++i) {
     if (!std::strcmp(argv[i], "--threads") && i + 1 < argc) threads = std::atoi(argv[++i]);
     else if (!std::strcmp(argv[i], "--v2")) force = 2;
+    else if (!std::strcmp(argv[i], "--raw")) raw = true;
     else if (!std::strcmp(argv[i], "--gpu")) gpu = (i + 1 < argc && argv[i + 1][0] != '-') ? std::atoi(argv[++i]) : 0;
     else {
       std::fprintf(stderr, "encoder: unknown option %s\n", argv[i]);
@@ -87,6 +89,28 @@ int main(int argc, char** argv) {
       return 1;
     }
     t2 = now_ms();
+  }
+  if (raw) {  // same code and payload words, no gap array
+    gh_stream st;
+    if (gh_stream_parse(out.data(), out.size(), &st)) {
+      std::fprintf(stderr, "encoder: %s\n", gh_last_error());
+      return 1;
+    }
+    std::vector<uint8_t> r;
+    auto put = [&](uint64_t x) {
+      for (int i = 0; i < 8; ++i) r.push_back((uint8_t)(x >> (8 * i)));
+    };
+    put(GH_RAW_MAGIC);
+    put(st.nsyms);
+    for (uint32_t i = 0; i < st.nsyms; ++i) {
+      r.push_back(st.syms[i].symbol);
+      r.push_back(st.syms[i].length);
+    }
+    put(st.n);
+    put(st.w);
+    const uint8_t* pw = (const uint8_t*)st.payload;
+    r.insert(r.end(), pw, pw + 4 * st.w);
+    out.swap(r);
   }
   FILE* o = std::fopen(argv[2], "wb");
   if (!o) {

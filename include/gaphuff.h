@@ -246,6 +246,17 @@ typedef struct gh_sync_report {
  * counter back).  rep may be NULL. */
 int gh_sync_gaps(int device, const gh_sym* syms, uint32_t nsyms, const uint32_t* d_words,
                  uint64_t w, uint32_t* d_gap_words, void* hip_stream, gh_sync_report* rep);
+/* Raw-stream file container (this repo's; gpuhd keeps its streams in memory,
+ * demo.cc:100-160): u64 GH_RAW_MAGIC ("GHRAW1\0\0"), u64 nsyms, nsyms x {u8 symbol,
+ * u8 length} in code order, u64 N, u64 W, W x u32 units (codewords MSB-first). */
+#define GH_RAW_MAGIC 0x0000315741524847ull
+typedef struct gh_raw_stream {
+  const gh_sym* syms;
+  uint32_t nsyms;
+  uint64_t n, w;
+  const uint32_t* units;   /* view into the file image                             */
+} gh_raw_stream;
+int gh_raw_parse(const void* file, size_t file_len, gh_raw_stream* out);
 /* gh_ctx_load for a raw stream held in host memory: uploads words[0..w), builds its
  * gap array with gh_sync_gaps and loads the whole stream (n output bytes) into ctx;
  * gh_ctx_decode / gh_ctx_report / gh_ctx_download then work as for a gap-array file. */

@@ -241,3 +241,41 @@ def test_gpu_sync_random_codes(gpu, orc, seed):
     gaps, _ = _sync_on_gpu(gpu, units, syms)
     assert np.array_equal(gaps, orc.raw_gaps(d, syms))
     assert np.array_equal(gpu.decode_raw(units, syms, n), d)
+
+
+BIN = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bin")
+
+
+@pytest.mark.skipif(not os.access(os.path.join(BIN, "encoder"), os.X_OK), reason="CLIs not built")
+@pytest.mark.parametrize("r,n", [(0.5, 100_003), (0.9, 1), (0.5, 0)])
+def test_cli_encoder_raw_container(orc, gh, tmp_path, r, n):
+    """bin/encoder --raw: same code and payload as the gap-array file, no gaps."""
+    import subprocess
+    d = orc.generate(8, r, n)
+    d.tofile(tmp_path / "d.bin")
+    subprocess.run([os.path.join(BIN, "encoder"), str(tmp_path / "d.bin"), str(tmp_path / "d.raw"), "--raw"],
+                   check=True, capture_output=True, timeout=60)
+    syms, n2, units = gh.parse_raw(np.fromfile(tmp_path / "d.raw", dtype=np.uint8))
+    assert n2 == n and syms == orc.symbols_of(d) if n else n2 == 0
+    if n:
+        assert np.array_equal(units, orc.raw_encode(d, syms))
+
+
+def test_raw_parse_rejects_bad(gh):
+    with pytest.raises(gh.GapHuffError):
+        gh.parse_raw(b"GHRAW1\x00\x00" + b"\x00" * 4)
+    with pytest.raises(gh.GapHuffError):
+        gh.parse_raw(b"\x01" * 64)
+
+
+@pytest.mark.gpu
+def test_gpu_cli_decoder_raw_container(gpu, orc, tmp_path):
+    import subprocess
+    d = orc.generate(9, 0.5, 2_000_003)
+    d.tofile(tmp_path / "d.bin")
+    subprocess.run([os.path.join(BIN, "encoder"), str(tmp_path / "d.bin"), str(tmp_path / "d.raw"), "--raw"],
+                   check=True, capture_output=True, timeout=60)
+    r = subprocess.run([os.path.join(BIN, "decoder"), str(tmp_path / "d.raw"), str(tmp_path / "o.bin"),
+                        "--verify", str(tmp_path / "d.bin")], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "Raw stream" in r.stdout and "Verification: PASS" in r.stdout
