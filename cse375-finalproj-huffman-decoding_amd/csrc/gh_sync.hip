@@ -35,8 +35,9 @@
 //                      first pass finds none.
 //  gh_sync_pack_kernel after repairs: pairs -> gap words.
 //
-// One 12-bit LUT in LDS serves both walks: {length of the first codeword (0 if > 12
-// bits), bits of the complete codewords that fit in the 12 bits}.  Walks take the
+// One 12-bit LUT in LDS serves both walks: {step (the advance below, or the first
+// length when no codeword fits), length of the first codeword (0 if > 12 bits), bits of
+// the complete codewords that fit in the 12 bits (the advance)}.  Walks take the
 // multi-codeword step except where a step could skip the start that has to be
 // recorded; codes of 13-16 bits use four canonical thresholds.
 #include <hip/hip_runtime.h>
@@ -68,7 +69,7 @@ struct SyncParams {
   const uint32_t* words;  // raw stream, 16-byte aligned
   uint64_t w;             // words
   uint64_t g;             // segments = ceil(w / 4)
-  const uint16_t* lut;    // 1 << SK entries {first len, multi-codeword advance << 5}
+  const uint16_t* lut;    // 1 << SK entries {step, first len << 5, multi-codeword advance << 10}
   uint32_t t13, t14, t15, t16;  // canonical left-aligned limits of lengths 13..16
   uint32_t* gaps;         // ceil(g / 8) gap words
   uint32_t* pairs;        // g bytes {a | b << 4}, as words
@@ -101,10 +102,16 @@ __device__ __forceinline__ uint32_t walk_word(uint32_t hi, uint32_t lo, uint32_t
   while (off < 32) {
     const uint32_t p16 = (uint32_t)((win << off) >> 48);
     const uint32_t e = lut[p16 >> (16 - SK)];
-    const uint32_t adv = e >> 5;
-    uint32_t len = e & 31u;
-    if (LONG && len == 0) len = long_len(p16, p);
-    off += (adv != 0 && (!BOUND || off + SK <= 32)) ? adv : len;
+    if constexpr (!BOUND) {
+      uint32_t st = e & 31u;  // precomputed: advance if any, else the first length
+      if (LONG && st == 0) st = long_len(p16, p);
+      off += st;
+    } else {
+      const uint32_t adv = e >> 10;
+      uint32_t len = (e >> 5) & 31u;
+      if (LONG && len == 0) len = long_len(p16, p);
+      off += (adv != 0 && off + SK <= 32) ? adv : len;
+    }
   }
   return off - 32;
 }
@@ -327,7 +334,10 @@ void build_sync_tables(const Canon& c, SyncTables& st) {
     // a prefix outside the code space (only met by walks that started mid-codeword)
     // steps one bit, like long_len's fallback
     if (first == 0 && (v << (16 - SK)) >= st.T[GH_MAX_CODE_LEN]) first = 1;
-    st.lut[v] = (uint16_t)(first | (s << 5));
+    // {step = advance, or the first length when no codeword fits (0: a long code),
+    //  first length << 5, advance << 10}
+    const uint32_t step = s ? s : first;
+    st.lut[v] = (uint16_t)(step | (first << 5) | (s << 10));
   }
 }
 
