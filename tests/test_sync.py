@@ -279,3 +279,27 @@ def test_gpu_cli_decoder_raw_container(gpu, orc, tmp_path):
                         "--verify", str(tmp_path / "d.bin")], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert "Raw stream" in r.stdout and "Verification: PASS" in r.stdout
+
+
+def test_raw_parse_fuzz(gh, orc):
+    """Truncated / corrupted raw containers: an error or a valid parse, never a crash."""
+    rng = np.random.default_rng(3)
+    d = orc.generate(2, 0.5, 5000)
+    syms = orc.symbols_of(d)
+    units = orc.raw_encode(d, syms)
+    hdr = np.concatenate([np.frombuffer(np.uint64(0x0000315741524847).tobytes(), np.uint8),
+                          np.frombuffer(np.uint64(len(syms)).tobytes(), np.uint8),
+                          np.array([x for e in syms for x in e], np.uint8),
+                          np.frombuffer(np.array([d.size, units.size], np.uint64).tobytes(), np.uint8),
+                          units.view(np.uint8)])
+    s2, n2, u2 = gh.parse_raw(hdr)
+    assert s2 == syms and n2 == d.size and np.array_equal(u2, units)
+    for _ in range(300):
+        b = hdr[: int(rng.integers(0, hdr.size + 1))].copy()
+        for _ in range(int(rng.integers(0, 4))):
+            if b.size:
+                b[int(rng.integers(0, min(b.size, 600)))] = int(rng.integers(0, 256))
+        try:
+            gh.parse_raw(b)
+        except gh.GapHuffError:
+            pass
