@@ -303,3 +303,17 @@ def test_raw_parse_fuzz(gh, orc):
             gh.parse_raw(b)
         except gh.GapHuffError:
             pass
+
+
+def test_sync_gaps_argument_checks(gh):
+    """Checked before any device work (so they run without a GPU)."""
+    with pytest.raises(gh.GapHuffError) as e:
+        gh.sync_gaps([(65, 1), (66, 1)], 4, 8, 1 << 20)  # d_words not 16-byte aligned
+    assert e.value.code == -1
+    with pytest.raises(gh.GapHuffError) as e:
+        gh.sync_gaps([(65, 2), (66, 1)], 1 << 20, 8, 1 << 20)  # lengths not canonical order
+    assert e.value.code == -3
+    with pytest.raises(gh.GapHuffError) as e:
+        gh.sync_gaps([(65, 1), (66, 1), (67, 1)], 1 << 20, 8, 1 << 20)  # Kraft sum > 1
+    assert e.value.code == -3
+    assert gh.sync_gaps([(65, 1)], 1 << 20, 0, 1 << 20).g == 0  # empty stream: nothing to do
