@@ -35,11 +35,11 @@
 //                      first pass finds none.
 //  gh_sync_pack_kernel after repairs: pairs -> gap words.
 //
-// One 12-bit LUT in LDS serves both walks: {step (the advance below, or the first
-// length when no codeword fits), length of the first codeword (0 if > 12 bits), bits of
-// the complete codewords that fit in the 12 bits (the advance)}.  Walks take the
+// One 13-bit LUT in LDS serves both walks: {step (the advance below, or the first
+// length when no codeword fits), length of the first codeword (0 if > 13 bits), bits of
+// the complete codewords that fit in the 13 bits (the advance)}.  Walks take the
 // multi-codeword step except where a step could skip the start that has to be
-// recorded; codes of 13-16 bits use four canonical thresholds.
+// recorded; codes of 14-16 bits use the canonical thresholds.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -53,7 +53,7 @@
 namespace gh {
 namespace {
 
-constexpr int SK = 12;          // LUT prefix bits
+constexpr int SK = 13;          // LUT prefix bits (12: cfg4 2.28 ms, 13: 2.08, 14: 3.10 - occupancy)
 constexpr int SYNC_TB = 256;    // threads per workgroup
 constexpr uint32_t SYNC_CHAIN = 256;  // segments one repair chain may walk per pass
 constexpr int SYNC_HALO = 8;          // warm-up segments per wave (GH_SYNC_HALO overrides)
