@@ -2182,6 +2182,8 @@ struct gh_ctx {
   int tb = TB;           // workgroup size of the loaded path
   size_t lut_bytes = 0;  // LDS bytes of the decode LUT of the loaded path
   hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;  // recorded after every decode, on the stream it ran on
+  bool done_rec = false;
   int num_cu = 0;
   bool loaded = false;
   Canon canon;
@@ -2449,6 +2451,7 @@ extern "C" int gh_ctx_create(int device, gh_ctx** out) {
   c->num_cu = prop.multiProcessorCount;
   GH_HIP(hipSetDevice(device));
   GH_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  GH_HIP(hipEventCreateWithFlags(&c->done, hipEventDisableTiming));
   GH_HIP(hipMalloc(&c->d_misc, 128));
   GH_HIP(hipMemset(c->d_misc, 0, 128));
   for (bool sg : {false, true})
@@ -2497,6 +2500,7 @@ extern "C" int gh_ctx_destroy(gh_ctx* c) {
     (void)hipEventDestroy(e.first);
     (void)hipEventDestroy(e.second);
   }
+  if (c->done) (void)hipEventDestroy(c->done);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return GH_OK;
@@ -2825,6 +2829,8 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
   GH_HIP(hipSetDevice(c->device));
   if (c->nseg == 0) {
     GH_HIP(hipMemsetAsync(c->d_misc + 2, 0, 8, st));
+    GH_HIP(hipEventRecord(c->done, st));
+    c->done_rec = true;
     return GH_OK;
   }
   if (++c->epoch >= EPOCH_MAX) {  // granule epochs wrap: start clean
@@ -2982,6 +2988,15 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     GH_HIP(hipEventRecord(ev.second, st));
     c->pending.push_back(ev);
   }
+  GH_HIP(hipEventRecord(c->done, st));
+  c->done_rec = true;
+  return GH_OK;
+}
+
+// Waits for the context's last decode, whatever stream it was launched on.
+static int wait_decode(gh_ctx* c) {
+  GH_HIP(hipStreamSynchronize(c->stream));
+  if (c->done_rec) GH_HIP(hipEventSynchronize(c->done));
   return GH_OK;
 }
 
@@ -2990,6 +3005,7 @@ extern "C" int gh_ctx_report(gh_ctx* c, void* hip_stream, gh_report* rep) {
   hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
   GH_HIP(hipSetDevice(c->device));
   GH_HIP(hipStreamSynchronize(st));
+  if (int rc = wait_decode(c)) return rc;
   for (auto& e : c->pending) {
     float ms = 0;
     GH_HIP(hipEventElapsedTime(&ms, e.first, e.second));
@@ -3033,7 +3049,7 @@ extern "C" int gh_ctx_download(gh_ctx* c, uint64_t off, uint8_t* dst, uint64_t n
   if (off + nbytes > c->out_cap) return fail(GH_E_ARG, "download beyond the output capacity");
   if (!nbytes) return GH_OK;
   GH_HIP(hipSetDevice(c->device));
-  GH_HIP(hipStreamSynchronize(c->stream));
+  if (int rc = wait_decode(c)) return rc;
   GH_HIP(hipMemcpy(dst, c->d_out + off, nbytes, hipMemcpyDeviceToHost));
   return GH_OK;
 }
@@ -3052,6 +3068,7 @@ extern "C" int gh_ctx_copy_output(gh_ctx* c, uint64_t off, void* dst, uint64_t n
   if (!nbytes) return GH_OK;
   hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
   GH_HIP(hipSetDevice(c->device));
+  if (c->done_rec) GH_HIP(hipStreamWaitEvent(st, c->done, 0));  // after the last decode
   GH_HIP(hipMemcpyAsync(dst, c->d_out + off, nbytes, hipMemcpyDefault, st));
   return GH_OK;
 }

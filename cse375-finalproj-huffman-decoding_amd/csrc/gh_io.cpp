@@ -58,8 +58,26 @@ struct Staging {
   void* buf[2] = {nullptr, nullptr};
   hipEvent_t ev[2] = {nullptr, nullptr};
   hipStream_t st = nullptr;
+  bool ready() const { return st && buf[0] && buf[1] && ev[0] && ev[1]; }
+  // Frees whatever a failed init() left (a set is pooled only when ready()).
+  void release() {
+    for (int i = 0; i < 2; ++i) {
+      if (ev[i]) (void)hipEventDestroy(ev[i]);
+      if (buf[i]) (void)hipHostFree(buf[i]);
+      ev[i] = nullptr;
+      buf[i] = nullptr;
+    }
+    if (st) (void)hipStreamDestroy(st);
+    st = nullptr;
+  }
   int init() {
-    if (st) return GH_OK;
+    if (ready()) return GH_OK;
+    release();
+    int rc = init_parts();
+    if (rc) release();
+    return rc;
+  }
+  int init_parts() {
     GH_HIPI(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     for (int i = 0; i < 2; ++i) {
       GH_HIPI(hipHostMalloc(&buf[i], IO_CHUNK, hipHostMallocDefault));
@@ -93,14 +111,10 @@ struct StagingLease {
     if (!s) return;
     std::lock_guard<std::mutex> g(g_pool_mu);
     Staging*& slot = g_pool[dev];
-    if (!slot) {
-      slot = s;  // keep one set per device
+    if (!slot && s->ready()) {
+      slot = s;  // keep one complete set per device
     } else {
-      for (int i = 0; i < 2; ++i) {
-        if (s->ev[i]) (void)hipEventDestroy(s->ev[i]);
-        if (s->buf[i]) (void)hipHostFree(s->buf[i]);
-      }
-      if (s->st) (void)hipStreamDestroy(s->st);
+      s->release();
       delete s;
     }
   }
@@ -314,6 +328,9 @@ extern "C" int gh_raw_parse(const void* file, size_t len, gh_raw_stream* out) {
   Canon c;
   int rc = build_canon(r.syms, r.nsyms, c);
   if (rc) return rc;
+  // every symbol takes at least minlen bits: N symbols cannot fit fewer units
+  if (r.n && (c.minlen == 0 || r.n > (32 * r.w) / c.minlen))
+    return fail(GH_E_FORMAT, "raw stream holds fewer bits than N symbols need");
   *out = r;
   return GH_OK;
 }

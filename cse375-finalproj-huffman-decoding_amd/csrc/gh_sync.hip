@@ -457,6 +457,13 @@ extern "C" int gh_ctx_load_raw(gh_ctx* ctx, const gh_sym* syms, uint32_t nsyms, 
   if (rc) return rc;
   GH_HIPS(hipSetDevice(dev));
   const uint64_t g = ceil_div(w, 4);
+  {  // N symbols of at least minlen bits each must fit the 32 w bits
+    Canon cn;
+    rc = build_canon(syms, nsyms, cn);
+    if (rc) return rc;
+    if (n && (cn.minlen == 0 || n > (32 * w) / cn.minlen))
+      return fail(GH_E_FORMAT, "raw stream holds fewer bits than N symbols need");
+  }
   DevBuf dw, dg;
   GH_HIPS(hipMalloc(&dw.p, 4 * (w + 16)));
   GH_HIPS(hipMemset(dw.p, 0, 4 * (w + 16)));

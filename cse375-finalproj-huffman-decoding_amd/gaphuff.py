@@ -48,7 +48,7 @@ EXPORTED = (
     "gh_ectx_create", "gh_ectx_destroy", "gh_ectx_load", "gh_ectx_plan", "gh_ectx_encode",
     "gh_ectx_download", "gh_ctx_device", "gh_sync_gaps", "gh_ctx_load_raw",
     "gh_ctx_load_file", "gh_ctx_save_file", "gh_dev_alloc", "gh_dev_free", "gh_dev_copy",
-    "gh_raw_parse",
+    "gh_raw_parse", "gh_bw_copy",
 )
 
 
@@ -161,6 +161,7 @@ def lib() -> ctypes.CDLL:
             "gh_dev_alloc": ([I, U64, ctypes.POINTER(P)], I),
             "gh_dev_free": ([P], I),
             "gh_dev_copy": ([P, P, U64], I),
+            "gh_bw_copy": ([P, P, U64, P, I, ctypes.POINTER(ctypes.c_float)], I),
             "gh_version": ([], ctypes.c_char_p),
             "gh_last_error": ([], ctypes.c_char_p),
         }
@@ -494,6 +495,15 @@ def sync_gaps(symbols: Sequence[tuple], d_words: int, w: int, d_gap_words: int, 
     return r
 
 
+def bw_copy(dst_ptr: int, src_ptr: int, nbytes: int, hip_stream: int = 0, reps: int = 10) -> float:
+    """Streaming-copy yardstick: ms per pass of a 16-B-lane copy of `nbytes` device
+    bytes (gh_bw_copy, include/gaphuff.h)."""
+    ms = ctypes.c_float()
+    _check(lib().gh_bw_copy(ctypes.c_void_p(dst_ptr), ctypes.c_void_p(src_ptr), nbytes,
+                            ctypes.c_void_p(hip_stream or None), reps, ctypes.byref(ms)))
+    return float(ms.value)
+
+
 def parse_raw(file_bytes):
     """Parse a raw-stream container (bin/encoder --raw): (symbols, n, units)."""
     raw = _u8(file_bytes)
@@ -515,6 +525,8 @@ def decode_raw(units, symbols: Sequence[tuple], n: int, device: int = 0) -> np.n
         rep = d.report()
         if rep.status:
             raise GapHuffError(-7, f"device status {rep.status}")
+        if rep.symbols < n:  # never hand back undecoded (uninitialised) output bytes
+            raise GapHuffError(-7, f"raw stream decoded to {rep.symbols} of {n} symbols")
         return d.download(n) if n else np.zeros(0, dtype=np.uint8)
 
 

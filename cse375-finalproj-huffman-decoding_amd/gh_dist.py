@@ -8,12 +8,19 @@ per-shard symbol counts.  The reference has no multi-GPU path (its launcher is
 single-device, decoder.cu:732-815); the north star adds an RCCL gather of the
 decoded shards to one rank as the last step, timed separately from the decode.
 
+One stream, many readers: rank 0 builds the compressed.huff once and writes it to a
+file (``share_stream``); every rank then streams only its own shard's words from that
+file (``gh_ctx_load_file``), so no rank holds the global stream in memory.
+
 Backend-agnostic: RCCL ("nccl") on the GPU box, gloo in the CPU tests.
 """
 from __future__ import annotations
 
+import os
 import time
-from typing import List, Optional, Tuple
+from typing import Callable, List, Optional, Tuple
+
+import numpy as np
 
 import gaphuff as gh
 
@@ -32,12 +39,52 @@ def shard_alg_bytes(w: int, begin: int, end: int, out_bytes: int) -> int:
     return 4 * pay + 4 * gaps + out_bytes
 
 
+def _bcast_ints(dist, vals: List[int], device) -> List[int]:
+    import torch
+
+    t = torch.tensor(vals, dtype=torch.int64, device=device)
+    if dist is not None:
+        dist.broadcast(t, src=0)
+    return [int(x) for x in t.cpu()]
+
+
+def share_stream(dist, rank: int, path: str, make_image: Callable[[], np.ndarray],
+                 device) -> dict:
+    """Rank 0 builds the compressed.huff image (``make_image()``) and writes it to
+    `path`; every rank gets the header sizes.  Returns {n, w, g, version, file_bytes}.
+
+    The image goes to a temporary name first and is renamed when complete, so a reader
+    never sees a partial file.  Callers remove `path` after every rank has loaded."""
+    hdr = [0, 0, 0, 0, 0, 0]  # ok, n, w, g, version, file_bytes
+    if rank == 0:
+        try:
+            img = make_image()
+            s = gh.parse(img)
+            tmp = path + ".part"
+            img.tofile(tmp)
+            os.replace(tmp, path)
+            hdr = [1, s.n, s.w, s.g, s.version, int(img.size)]
+            del img, s
+        except Exception as ex:  # reported on every rank below
+            gh_err = repr(ex)
+            hdr = [0, 0, 0, 0, 0, 0]
+            if dist is None:
+                raise
+            print(f"[rank 0] share_stream failed: {gh_err}", flush=True)
+    ok, n, w, g, ver, fb = _bcast_ints(dist, hdr, device)
+    if not ok:
+        raise RuntimeError("rank 0 could not build the shared stream")
+    return {"n": n, "w": w, "g": g, "version": ver, "file_bytes": fb}
+
+
 def exclusive_offsets(dist, count: int, device) -> Tuple[int, List[int]]:
     """Output byte offset of this rank's shard (exclusive scan of shard sizes) and
     the list of all shard sizes, via one all_gather of one integer per rank."""
     import torch
 
     t = torch.tensor([count], dtype=torch.int64, device=device)
+    if dist is None:
+        return 0, [count]
     allv = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
     dist.all_gather(allv, t)
     sizes = [int(x.item()) for x in allv]
@@ -45,32 +92,49 @@ def exclusive_offsets(dist, count: int, device) -> Tuple[int, List[int]]:
     return sum(sizes[:rank]), sizes
 
 
+def verify_slice(got: np.ndarray, seed: int, redundancy: float, offset: int,
+                 threads: int = 0) -> bool:
+    """Shard output == the generator's bytes [offset, offset + len(got)) (the counter-
+    based generator makes any slice reproducible, so no rank needs the whole input)."""
+    want = gh.generate(seed, redundancy, got.size, offset=offset, threads=threads)
+    return bool(np.array_equal(got, want))
+
+
 def gather_to_root(dist, shard, nbytes: int, device) -> Tuple[Optional["torch.Tensor"], float]:
     """Gather every rank's decoded shard (uint8 tensor, first `nbytes` valid) to rank 0.
 
-    Returns (concatenated output on rank 0 / None elsewhere, elapsed ms of the
-    collective).  Shards are padded to the largest shard so one gather moves them."""
+    Rank 0 posts one receive per rank straight into its slice of one output buffer of
+    the exact total size; the other ranks send their `nbytes` (grouped point-to-point:
+    RCCL send/recv over xGMI on the GPU box).  Returns (the whole output on rank 0 /
+    None elsewhere, elapsed ms of the transfer)."""
     import torch
 
-    _, sizes = exclusive_offsets(dist, nbytes, device)
-    cap = max(1, max(sizes))
-    padded = torch.zeros(cap, dtype=torch.uint8, device=device)
-    if nbytes:
-        padded[:nbytes] = shard[:nbytes]
+    off, sizes = exclusive_offsets(dist, nbytes, device)
     rank, world = dist.get_rank(), dist.get_world_size()
-    bufs = [torch.empty(cap, dtype=torch.uint8, device=device) for _ in range(world)] \
-        if rank == 0 else None
+    total = sum(sizes)
+    full = torch.empty(max(1, total), dtype=torch.uint8, device=device) if rank == 0 else None
+    is_cuda = device is not None and torch.device(device).type == "cuda"
     dist.barrier()
-    if device is not None and torch.device(device).type == "cuda":
+    if is_cuda:
         torch.cuda.synchronize()
     t0 = time.perf_counter()
-    dist.gather(padded, bufs, dst=0)
-    if device is not None and torch.device(device).type == "cuda":
+    if rank == 0:
+        if nbytes:
+            full[:nbytes].copy_(shard[:nbytes])
+        ops = [dist.P2POp(dist.irecv, full[sum(sizes[:k]):sum(sizes[:k + 1])], k)
+               for k in range(1, world) if sizes[k]]
+    else:
+        ops = [dist.P2POp(dist.isend, shard[:nbytes], 0)] if nbytes else []
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    if is_cuda:
         torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3
+    dist.barrier()
     if rank != 0:
         return None, ms
-    return torch.cat([bufs[k][:sizes[k]] for k in range(world)]), ms
+    return full[:total], ms
 
 
 def reduce_max_sum(dist, values: List[float], device) -> Tuple[List[float], List[float]]:
@@ -94,3 +158,15 @@ def all_true(dist, ok: bool, device) -> bool:
     t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MIN)
     return bool(t.item())
+
+
+def host_threads() -> int:
+    """Host threads for generate/encode: OMP_NUM_THREADS when set (16 on the GPU
+    box), else the CPUs this process may run on, capped at 32."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return max(1, min(32, len(os.sched_getaffinity(0))))
+    except AttributeError:  # pragma: no cover
+        return max(1, min(32, os.cpu_count() or 1))

@@ -1,4 +1,7 @@
-// bin/decoder <compressed.huff | raw container> <output> [--gpus N] [--reps R] [--json] [--verify FILE]
+// bin/decoder <compressed.huff | raw container> <output> [--gpus N] [--shards S] [--reps R] [--json]
+//             [--verify FILE]
+// --shards S (default: one per GPU) splits the gap segments into S shards, shard k on
+// device k mod N, each streaming its own payload range and writing at its offset.
 // A raw-stream container (bin/encoder --raw, GH_RAW_MAGIC) is decoded by the
 // self-synchronising path (gh_ctx_load_raw) on one GPU.
 //
@@ -32,14 +35,15 @@ static int die(const char* what, int rc) {
 int main(int argc, char** argv) {
   if (argc < 3) {
     std::fprintf(stderr,
-                 "Usage: bin/decoder input output [--gpus N] [--reps R] [--json] [--verify FILE]\n");
+                 "Usage: bin/decoder input output [--gpus N] [--shards S] [--reps R] [--json] [--verify FILE]\n");
     return 2;
   }
-  int ngpus = 1, reps = 1;
+  int ngpus = 1, reps = 1, nshards = 0;
   bool json = false;
   const char* verify = nullptr;
   for (int i = 3; i < argc; ++i) {
     if (!std::strcmp(argv[i], "--gpus") && i + 1 < argc) ngpus = std::atoi(argv[++i]);
+    else if (!std::strcmp(argv[i], "--shards") && i + 1 < argc) nshards = std::atoi(argv[++i]);
     else if (!std::strcmp(argv[i], "--reps") && i + 1 < argc) reps = std::atoi(argv[++i]);
     else if (!std::strcmp(argv[i], "--json")) json = true;
     else if (!std::strcmp(argv[i], "--verify") && i + 1 < argc) verify = argv[++i];
@@ -65,11 +69,12 @@ int main(int argc, char** argv) {
     is_raw = std::fread(&magic, 1, 8, f) == 8 && magic == GH_RAW_MAGIC;
     std::fclose(f);
   }
-  if (is_raw) ngpus = 1;  // a raw stream's segment entries are found on one device
+  if (is_raw) ngpus = nshards = 1;  // a raw stream's segment entries are found on one device
   const int ndev = gh_device_count();
   if (ndev < 1) return die("no HIP device", GH_E_NODEV);
   if (ngpus > ndev) ngpus = ndev;
-  std::vector<gh_ctx*> ctx(ngpus, nullptr);
+  if (nshards < 1) nshards = ngpus;
+  std::vector<gh_ctx*> ctx(nshards, nullptr);
   auto cleanup = [&]() {
     for (auto* c : ctx) gh_ctx_destroy(c);
   };
@@ -77,7 +82,7 @@ int main(int argc, char** argv) {
   const double t0 = now_ms();
   gh_file_info info{};
   if ((rc = gh_ctx_create(0, &ctx[0]))) { cleanup(); return die("device init", rc); }
-  std::vector<uint64_t> bounds(ngpus + 1, 0);
+  std::vector<uint64_t> bounds(nshards + 1, 0);
   if (is_raw) {
     std::vector<uint8_t> file;
     FILE* f = std::fopen(argv[1], "rb");
@@ -99,7 +104,7 @@ int main(int argc, char** argv) {
     bounds[1] = info.g;
     std::printf("Raw stream: gap array built on the GPU in %.3f ms (%llu boundaries repaired)\n",
                 sr.kernel_ms, (unsigned long long)sr.mismatches);
-  } else if (ngpus == 1) {
+  } else if (nshards == 1) {
     if ((rc = gh_ctx_load_file(ctx[0], argv[1], 0, UINT64_MAX, 0, &info))) {
       cleanup();
       return die("bad compressed stream / upload", rc);
@@ -111,9 +116,9 @@ int main(int argc, char** argv) {
       cleanup();
       return die("bad compressed stream / upload", rc);
     }
-    gh_plan_shards(info.g, (uint32_t)ngpus, bounds.data());
-    for (int k = 0; k < ngpus; ++k) {
-      if (k && (rc = gh_ctx_create(k, &ctx[k]))) { cleanup(); return die("device init", rc); }
+    gh_plan_shards(info.g, (uint32_t)nshards, bounds.data());
+    for (int k = 0; k < nshards; ++k) {
+      if (k && (rc = gh_ctx_create(k % ngpus, &ctx[k]))) { cleanup(); return die("device init", rc); }
       if ((rc = gh_ctx_load_file(ctx[k], argv[1], bounds[k], bounds[k + 1], 0, nullptr))) {
         cleanup();
         return die("upload", rc);
@@ -128,13 +133,13 @@ int main(int argc, char** argv) {
   std::printf("Compressed size: %llu bytes\n", (unsigned long long)s.w);  // reference prints W
   const double t1 = now_ms();
   for (int r = 0; r < reps; ++r)
-    for (int k = 0; k < ngpus; ++k)
+    for (int k = 0; k < nshards; ++k)
       if ((rc = gh_ctx_decode(ctx[k], nullptr, 1))) { cleanup(); return die("decode", rc); }
-  std::vector<gh_report> rep(ngpus);
+  std::vector<gh_report> rep(nshards);
   float dec_ms = 0;
   uint32_t status = 0;
   uint64_t total = 0;
-  for (int k = 0; k < ngpus; ++k) {
+  for (int k = 0; k < nshards; ++k) {
     if ((rc = gh_ctx_report(ctx[k], nullptr, &rep[k]))) { cleanup(); return die("decode", rc); }
     dec_ms = std::max(dec_ms, rep[k].kernel_ms);
     status |= rep[k].status;
@@ -154,7 +159,12 @@ int main(int argc, char** argv) {
   // D2H -> pwrite); the reference always wrote "decodedfile" (huff.cpp:32)
   const double t2 = now_ms();
   uint64_t off = 0;
-  for (int k = 0; k < ngpus; ++k) {
+  for (int k = 0; k < nshards; ++k) {
+    if (k + 1 < nshards && rep[k].symbols > rep[k].out_bytes) {
+      cleanup();
+      std::fprintf(stderr, "decoder: shard %d overflowed its output (corrupted stream?)\n", k);
+      return 1;
+    }
     const uint64_t want = off < s.n ? std::min<uint64_t>(rep[k].symbols, s.n - off) : 0;
     if ((rc = gh_ctx_save_file(ctx[k], argv[2], off, 0, want, k == 0, nullptr))) {
       cleanup();

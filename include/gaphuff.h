@@ -285,6 +285,13 @@ int gh_dev_alloc(int device, uint64_t bytes, void** out);
 int gh_dev_free(void* p);
 int gh_dev_copy(void* dst, const void* src, uint64_t bytes);
 
+/* Diagnostic yardstick: one streaming copy of `bytes` (multiple of
+ * 16, 16-byte aligned device buffers) on `hip_stream` (NULL = default stream) of the
+ * current device, repeated `reps` times after one warm-up pass; *ms_avg = HIP-event
+ * time per pass.  The decode's roofline is quoted as a fraction of this rate.  No
+ * reference counterpart (the reference measures nothing on the device). */
+int gh_bw_copy(void* dst, const void* src, uint64_t bytes, void* hip_stream, int reps, float* ms_avg);
+
 /* Number of visible HIP devices (0 when none / no driver). */
 int gh_device_count(void);
 /* Library version string. */

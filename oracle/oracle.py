@@ -187,14 +187,24 @@ _PAR_RE = re.compile(r"Decompression time \(Parallel Decode\):\s+(\d+) us")
 _VER_RE = re.compile(r"Verification:\s+(PASS|FAIL)")
 
 
-def run_reference_cpu(name: str, data: np.ndarray, timeout: float = 600.0) -> dict:
+def run_reference_cpu(name: str, data: np.ndarray, timeout: float = 600.0,
+                      threads: Optional[int] = None) -> dict:
     """Run a reference CPU program (compiled from its own source) on `data`.
 
     sequential / parallel_cpu_prescan read data100_100.bin, parallel_decomp_cpu
     reads data.bin (sequential.cpp:240, parallel_cpu_prescan.cpp:596,
     parallel_cpu_decomp.cpp:655); each times decode() only and verifies.
+    `threads` (prescan / decomp only) runs the reference's main() through our
+    driver (_ref/prescan_driver, _ref/decomp_driver) with its hard-coded
+    ``thread_count`` (parallel_cpu_prescan.cpp:25, parallel_cpu_decomp.cpp:24)
+    set to that value; None runs the program as shipped.
     Returns {decode_us, verified, threads, wall_s}."""
-    exe = os.path.join(REF, name)
+    shipped = {"sequential": 1, "parallel_decomp_cpu": 1, "parallel_cpu_prescan": 16}
+    drivers = {"parallel_decomp_cpu": "decomp_driver", "parallel_cpu_prescan": "prescan_driver"}
+    exe_name, argv = name, []
+    if threads is not None and name in drivers:
+        exe_name, argv = drivers[name], [str(int(threads))]
+    exe = os.path.join(REF, exe_name)
     if not os.access(exe, os.X_OK):
         raise FileNotFoundError(exe)
     infile = "data.bin" if name == "parallel_decomp_cpu" else "data100_100.bin"
@@ -202,15 +212,14 @@ def run_reference_cpu(name: str, data: np.ndarray, timeout: float = 600.0) -> di
     try:
         _u8(data).tofile(os.path.join(td, infile))
         t0 = time.time()
-        r = subprocess.run([exe], cwd=td, capture_output=True, text=True, timeout=timeout)
+        r = subprocess.run([exe, *argv], cwd=td, capture_output=True, text=True, timeout=timeout)
         wall = time.time() - t0
         m = (_SEQ_RE if name == "sequential" else _PAR_RE).search(r.stdout)
         v = _VER_RE.search(r.stdout)
         if not m:
             raise RuntimeError(f"{name} produced no timing: {r.stdout[-400:]} {r.stderr[-400:]}")
-        threads = {"sequential": 1, "parallel_decomp_cpu": 1, "parallel_cpu_prescan": 16}[name]
         return {"decode_us": int(m.group(1)), "verified": bool(v and v.group(1) == "PASS"),
-                "threads": threads, "wall_s": wall}
+                "threads": int(threads) if argv else shipped[name], "wall_s": wall}
     finally:
         shutil.rmtree(td, ignore_errors=True)
 

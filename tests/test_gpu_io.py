@@ -71,15 +71,57 @@ def test_gpu_load_file_empty_and_truncated(gpu, tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("gpus", [1, 2])
-def test_gpu_cli_streaming_verify(gpu, tmp_path, gpus):
+@pytest.mark.parametrize("gpus,shards", [(1, 0), (2, 0), (1, 3), (1, 8)])
+def test_gpu_cli_streaming_verify(gpu, tmp_path, gpus, shards):
+    """bin/decoder on one or more devices (clamped to the visible ones) and with S
+    shards on them (--shards: shard k on device k mod N), each shard streaming its
+    payload range and writing at its offset of the output file."""
     if not os.access(os.path.join(BIN, "decoder"), os.X_OK):
         pytest.fail("bin/decoder not built")
     d, path = _write(tmp_path, gpu, 6, 0.1, 40_000_003)
     (tmp_path / "orig.bin").write_bytes(d.tobytes())
     out = str(tmp_path / "dec.bin")
-    r = subprocess.run([os.path.join(BIN, "decoder"), path, out, "--gpus", str(gpus), "--verify",
+    extra = ["--shards", str(shards)] if shards else []
+    r = subprocess.run([os.path.join(BIN, "decoder"), path, out, "--gpus", str(gpus), *extra, "--verify",
                         str(tmp_path / "orig.bin")], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert "Verification: PASS" in r.stdout
     assert np.array_equal(np.fromfile(out, dtype=np.uint8), d)
+
+
+@pytest.mark.gpu
+def test_decode_on_caller_stream_then_save_and_download(gpu, tmp_path):
+    """A decode launched on a caller's stream (as bench.py does with torch's stream) is
+    waited for by save_file / download / copy_output on the context's own stream
+    (gh_ctx completion event), with no synchronisation by the caller."""
+    import torch
+    d, path = _write(tmp_path, gpu, 8, 0.1, 30_000_001)
+    s = torch.cuda.Stream()
+    with gpu.Decoder(0) as dec:
+        dec.load_file(path)
+        for _ in range(3):
+            dec.decode(s.cuda_stream, timed=True)
+        out = str(tmp_path / "o.bin")
+        dec.save_file(out, d.size)  # no caller sync before this
+        assert np.array_equal(np.fromfile(out, dtype=np.uint8), d)
+        dec.decode(s.cuda_stream, timed=True)
+        assert np.array_equal(dec.download(d.size), d)
+        dec.decode(s.cuda_stream, timed=True)
+        t = torch.empty(d.size, dtype=torch.uint8, device="cuda")
+        dec.copy_output(t.data_ptr(), d.size)  # context stream, ordered after the decode
+        rep = dec.report()
+        assert rep.status == 0 and rep.launches == 5
+        assert np.array_equal(t.cpu().numpy(), d)
+
+
+@pytest.mark.gpu
+def test_raw_stream_shorter_than_n_is_an_error(gpu):
+    """decode_raw must not return undecoded bytes when the stream holds fewer than N
+    symbols: the size check rejects it before any decode."""
+    import oracle
+    data = gpu.generate(9, 0.5, 10_000)
+    syms = oracle.symbols_of(data)
+    units = oracle.raw_encode(data, syms)
+    with pytest.raises(gpu.GapHuffError):
+        gpu.decode_raw(units, syms, 40_000)
+    assert np.array_equal(gpu.decode_raw(units, syms, data.size), data)

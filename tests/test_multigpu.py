@@ -1,7 +1,9 @@
 """N>1 path on CPU: gap-segment sharding, shard offsets, gather to rank 0 (gloo).
 
-Each rank builds the same global stream with the product encoder, takes its shard
-from gh_dist.shard_range, and stands in for the GPU shard decode with the CPU oracle
+Rank 0 builds the global stream once and shares it as a file (gh_dist.share_stream,
+as bench.py does under /dev/shm); each rank takes its shard from
+gh_dist.shard_range, checks it against the generator's slice at its output offset
+(gh_dist.verify_slice), and stands in for the GPU shard decode with the CPU oracle
 (bit-serial decode of the stream, sliced at the shard's segment-count offsets) —
 the oracle is the checker here, not the thing measured.  The collectives are the
 ones bench.py runs over RCCL on the GPU box (gh_dist)."""
@@ -21,7 +23,7 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, n, r, q):
+def _worker(rank, world, port, n, r, path, q):
     import sys
     for p in (os.path.join(ROOT, "cse375-finalproj-huffman-decoding_amd"), os.path.join(ROOT, "oracle")):
         sys.path.insert(0, p)
@@ -35,11 +37,14 @@ def _worker(rank, world, port, n, r, q):
     try:
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                                 world_size=world)
-        data = gh.generate(375, r, n)
-        img = gh.encode(data, threads=2)
-        s = gh.parse(img)
-        b, e = gh_dist.shard_range(s.g, world, rank)
-        counts = [oracle.segment_count(img, i) for i in range(s.g)]
+        # rank 0 builds the global stream once; the others only learn its header
+        hdr = gh_dist.share_stream(dist, rank, path,
+                                   lambda: gh.encode(gh.generate(375, r, n), threads=2), "cpu")
+        assert hdr["n"] == n
+        b, e = gh_dist.shard_range(hdr["g"], world, rank)
+        img = np.fromfile(path, dtype=np.uint8)
+        assert img.size == hdr["file_bytes"]
+        counts = [oracle.segment_count(img, i) for i in range(hdr["g"])]
         full, _ = oracle.decode(img)
         # the last segment may decode tail padding bits: outputs clamp at N
         lo, hi = min(sum(counts[:b]), n), min(sum(counts[:e]), n)
@@ -47,12 +52,17 @@ def _worker(rank, world, port, n, r, q):
         off, sizes = gh_dist.exclusive_offsets(dist, hi - lo, "cpu")
         assert off == lo, (off, lo)
         assert sum(sizes) == n
+        assert gh_dist.verify_slice(shard.numpy(), 375, r, off)
+        if hi > lo:  # a corrupted shard must fail its slice check
+            bad = shard.numpy().copy()
+            bad[-1] ^= 1
+            assert not gh_dist.verify_slice(bad, 375, r, off)
         mx, sm = gh_dist.reduce_max_sum(dist, [float(rank), float(hi - lo)], "cpu")
         assert mx[0] == world - 1 and sm[1] == n
         out, ms = gh_dist.gather_to_root(dist, shard, hi - lo, "cpu")
         ok = True
         if rank == 0:
-            ok = out is not None and np.array_equal(out.numpy(), data)
+            ok = out is not None and np.array_equal(out.numpy(), gh.generate(375, r, n))
         else:
             ok = out is None
         ok = gh_dist.all_true(dist, ok, "cpu")
@@ -63,12 +73,13 @@ def _worker(rank, world, port, n, r, q):
         q.put((rank, False, -1, -1, repr(ex)))
 
 
-@pytest.mark.parametrize("world,n,r", [(2, 40000, 0.5), (3, 25000, 0.1), (2, 5, 0.9)])
-def test_sharded_gather_gloo(world, n, r):
+@pytest.mark.parametrize("world,n,r", [(2, 40000, 0.5), (3, 25000, 0.1), (2, 5, 0.9), (4, 3000, 0.5)])
+def test_sharded_gather_gloo(world, n, r, tmp_path):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(k, world, port, n, r, q)) for k in range(world)]
+    path = str(tmp_path / "shared.huff")
+    procs = [ctx.Process(target=_worker, args=(k, world, port, n, r, path, q)) for k in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(world)]

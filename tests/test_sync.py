@@ -126,10 +126,32 @@ def test_gpu_sync_gaps_match_oracle(gpu, orc, r, n):
 
 @pytest.mark.gpu
 def test_gpu_sync_long_codes(gpu, orc):
-    """Codes of 13-16 bits (the threshold path) from the geometric fixture."""
+    """Codes longer than the 13-bit sync LUT (SK = 13, gh_sync.hip: the LONG kernels'
+    canonical-threshold path), up to 16 bits, from the geometric fixture."""
     d = _bin("geometric_long_codes")
     syms = orc.symbols_of(d)
-    assert max(l for _, l in syms) > 12
+    assert max(l for _, l in syms) > SYNC_LUT_BITS
+    units = orc.raw_encode(d, syms)
+    gaps, _ = _sync_on_gpu(gpu, units, syms)
+    assert np.array_equal(gaps, orc.raw_gaps(d, syms))
+    assert np.array_equal(gpu.decode_raw(units, syms, d.size), d)
+
+
+SYNC_LUT_BITS = 13  # SK in csrc/gh_sync.hip
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("maxlen", [SYNC_LUT_BITS, SYNC_LUT_BITS + 1])
+def test_gpu_sync_lut_boundary_codes(gpu, orc, maxlen):
+    """Complete codes whose longest codeword is exactly SK bits (fits the LUT: plain
+    kernel) and exactly SK + 1 bits (the LONG kernel): lengths 1, 2, ..., maxlen-1,
+    maxlen, maxlen (Kraft sum 1), symbols drawn with probability 2^-length."""
+    lens = list(range(1, maxlen)) + [maxlen, maxlen]
+    syms = [(40 + i, l) for i, l in enumerate(lens)]
+    p = np.array([2.0 ** -l for l in lens])
+    rng = np.random.default_rng(maxlen)
+    d = rng.choice(np.array([s for s, _ in syms], dtype=np.uint8), size=400_000, p=p / p.sum())
+    assert max(l for _, l in syms) == maxlen
     units = orc.raw_encode(d, syms)
     gaps, _ = _sync_on_gpu(gpu, units, syms)
     assert np.array_equal(gaps, orc.raw_gaps(d, syms))
