@@ -29,6 +29,9 @@
 //     past N, decoder.cu:672-728).
 #include <hip/hip_runtime.h>
 
+#include <map>
+#include <mutex>
+
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -1237,6 +1240,9 @@ constexpr int STAGE_PAD = 16;  // staging byte STAGE_PAD + i = tile byte i
 #ifndef GH_TILE_LAG3
 #define GH_TILE_LAG3 0         // grouped path: copy out at lag 3 (measured no faster than lag 2)
 #endif
+#ifndef GH_TILE_TOPCOPY
+#define GH_TILE_TOPCOPY 0      // with LAG3: copy tile k-3 out at the top of iteration k, before the decode
+#endif
 #ifndef GH_LB_MIDG
 #define GH_LB_MIDG 2           // decode group after which the round leader loads aggregates
 #endif
@@ -1667,6 +1673,7 @@ void gh_tile_kernel(const TileParams p) {
   // the next and copied out two iterations later (lag 3: two iterations of slack for
   // its prefix); multi path: staged at once (emit pass), copied out at lag 2.
   constexpr bool LAG3 = GH_TILE_LAG3 && !MULTI;
+  constexpr bool TOP = LAG3 && GH_TILE_TOPCOPY;  // copy-out before the decode (prefix two iterations old)
   uint32_t t1 = NONE, t2 = NONE, t3 = NONE;  // tiles of iterations k-1, k-2, k-3
   uint32_t tot1 = 0, tot2 = 0, tot3 = 0;     // their totals
   uint32_t buf = 0;               // k & 1
@@ -1706,7 +1713,7 @@ void gh_tile_kernel(const TileParams p) {
       la[j] = 0;
     }
     auto mid = [&]() {
-      if (have2 && lane == 0) {
+      if (!TOP && have2 && lane == 0) {
         const uint32_t r2 = tx / G;
         gp = __hip_atomic_load(&p.plocal[tx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         gr = r2 == 0 ? 0ull
@@ -1718,6 +1725,42 @@ void gh_tile_kernel(const TileParams p) {
           la[j] = __hip_atomic_load(&p.granules[lvalid[j] ? lt + j : 0], __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
     };
+    auto copy_block = [&]() {
+    // ---- copy tile k-2 out (its prefix was published about an iteration ago) -------
+    if (have2) {
+      unsigned long long goff = 0;
+      if (ABLATE(32)) {  // diagnostic: no prefix wait (wrong offsets)
+        goff = (unsigned long long)tx * 16000ull;
+      } else if (lane == 0) {
+        const uint32_t r2 = tx / G;
+        if (!granule_ok(p, gp, 2)) {
+          if (p.stats && wid == 0) atomicAdd(p.stats, 1ull);
+          gp = poll_granule(p, &p.plocal[tx], 2);
+        }
+        if (r2 > 0 && !granule_ok(p, gr, 2)) {
+          if (p.stats && wid == 0) atomicAdd(p.stats + 1, 1ull);
+          gr = poll_granule(p, &p.rprefix[r2], 2);
+        }
+        goff = (gp & VMASK) + (r2 > 0 ? (gr & VMASK) : 0ull);
+        if (wid == 0 && tx == p.ntiles - 1) *p.total = goff + (LAG3 ? tot3 : tot2);
+      }
+      goff = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(goff >> 32)) << 32) |
+             __builtin_amdgcn_readfirstlane((uint32_t)goff);
+      STAMP(6);
+      const uint32_t n2 =
+          goff >= p.out_cap ? 0u : (uint32_t)min<unsigned long long>(LAG3 ? tot3 : tot2, p.out_cap - goff);
+      if (!ABLATE(2)) copy_out_tile<TB>(p.out, p.lut_bytes + (LAG3 ? buf ^ 1u : buf) * p.stage_bytes, goff, n2, tid,
+                                      (uint32_t)ABLATE(0xFFFFFFFFu));
+    }
+    };
+    if constexpr (TOP) {
+      if (have2 && lane == 0) {  // published two iterations ago: almost always there
+        const uint32_t r2 = tx / G;
+        gp = __hip_atomic_load(&p.plocal[tx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        gr = r2 == 0 ? 0ull : __hip_atomic_load(&p.rprefix[r2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      copy_block();
+    }
     // ---- decode this tile (its words were loaded during the previous iteration) --
     const uint32_t seg0 = cur * (uint32_t)(U * TB) + (uint32_t)tid;
     uint32_t ow[MULTI ? 1 : U][MULTI ? 1 : OW], cnt[U];
@@ -1755,9 +1798,7 @@ void gh_tile_kernel(const TileParams p) {
         start[u] = seg == 0 ? (int)p.first_start : (int)((gw[u] >> (4 * nib)) & 15u);
         make_ewin(w[u], w4[u], start[u], S, e[u]);
       }
-#if !GH_PREFETCH_LATE
-      load(nxt);  // prefetch the next iteration's tile
-#endif
+      if constexpr (TOP || !GH_PREFETCH_LATE) load(nxt);  // prefetch the next iteration's tile
       if (have_cur && ABLATE(8)) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -1779,36 +1820,9 @@ void gh_tile_kernel(const TileParams p) {
       }
     }
     STAMP(0);
-    // ---- copy tile k-2 out (its prefix was published about an iteration ago) -------
-    if (have2) {
-      unsigned long long goff = 0;
-      if (ABLATE(32)) {  // diagnostic: no prefix wait (wrong offsets)
-        goff = (unsigned long long)tx * 16000ull;
-      } else if (lane == 0) {
-        const uint32_t r2 = tx / G;
-        if (!granule_ok(p, gp, 2)) {
-          if (p.stats && wid == 0) atomicAdd(p.stats, 1ull);
-          gp = poll_granule(p, &p.plocal[tx], 2);
-        }
-        if (r2 > 0 && !granule_ok(p, gr, 2)) {
-          if (p.stats && wid == 0) atomicAdd(p.stats + 1, 1ull);
-          gr = poll_granule(p, &p.rprefix[r2], 2);
-        }
-        goff = (gp & VMASK) + (r2 > 0 ? (gr & VMASK) : 0ull);
-        if (wid == 0 && tx == p.ntiles - 1) *p.total = goff + (LAG3 ? tot3 : tot2);
-      }
-      goff = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(goff >> 32)) << 32) |
-             __builtin_amdgcn_readfirstlane((uint32_t)goff);
-      STAMP(6);
-      const uint32_t n2 =
-          goff >= p.out_cap ? 0u : (uint32_t)min<unsigned long long>(LAG3 ? tot3 : tot2, p.out_cap - goff);
-      if (!ABLATE(2)) copy_out_tile<TB>(p.out, p.lut_bytes + (LAG3 ? buf ^ 1u : buf) * p.stage_bytes, goff, n2, tid,
-                                      (uint32_t)ABLATE(0xFFFFFFFFu));
-    }
+    if constexpr (!TOP) copy_block();
     STAMP(1);
-#if GH_PREFETCH_LATE
-    if constexpr (!MULTI) load(nxt);  // prefetch the next tile after the copy-out's waits
-#endif
+    if constexpr (!MULTI && !TOP && GH_PREFETCH_LATE) load(nxt);  // prefetch the next tile after the copy-out's waits
     uint32_t bpos[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -1938,6 +1952,7 @@ void gh_tile_kernel(const TileParams p) {
 }
 
 #include "gh_msplit.hip"
+#include "gh_wsplit.hip"
 #include "gh_gsplit.hip"
 
 // ============================================================================
@@ -2168,6 +2183,10 @@ struct gh_ctx {
   bool split = true;       // split mode (count / scan / write) vs the fused persistent kernel
   bool ms = false;         // lean multi-symbol split kernels (gh_msplit.hip)
   bool gs = false;         // grouped single-symbol split kernels (gh_gsplit.hip)
+  bool ws = false;         // wave-independent split kernels (gh_wsplit.hip)
+  uint32_t ws_nblocks = 0, ws_nranges = 0, ws_grid_c = 0;
+  unsigned long long* d_rng_tot = nullptr;
+  unsigned long long* d_rng_off = nullptr;
   uint32_t ms_k = 0;       // their LUT width
   int ms_wu = 2;           // their write kernel's chains per thread
   uint32_t ms_last_end = 0;  // end bit of the stream's last segment when the shard holds it
@@ -2227,6 +2246,11 @@ static void free_shard(gh_ctx* c) {
   (void)hipFree(c->d_lut_t);
   (void)hipFree(c->d_ms_lut_c);
   (void)hipFree(c->d_ms_lut_w);
+  (void)hipFree(c->d_rng_tot);
+  (void)hipFree(c->d_rng_off);
+  c->d_rng_tot = nullptr;
+  c->d_rng_off = nullptr;
+  c->ws = false;
   c->d_ms_lut_c = nullptr;
   c->d_ms_lut_w = nullptr;
   c->ms = false;
@@ -2276,10 +2300,8 @@ static MsKernels ms_kernels(uint32_t K, int wu) {
 // the K bits i: count LUT {b = their bits, end mask (bit e-1 per codeword end e)},
 // write LUT {their symbols (byte k = k-th), b | n << 8}.  Requires a complete code
 // with maxlen <= K, so every entry holds at least one codeword.
-static int ms_setup(gh_ctx* c) {
+static int ms_build_luts(gh_ctx* c, uint32_t K) {
   const Canon& cn = c->canon;
-  const char* ek = getenv("GH_MS_K");
-  const uint32_t K = (uint32_t)std::clamp(ek ? atoi(ek) : 10, (int)std::max<uint32_t>(cn.maxlen, 2), 12);
   std::vector<uint2> lc(1u << K), lw(1u << K);
   for (uint32_t i = 0; i < (1u << K); ++i) {
     const uint32_t bits = i << (32 - K);
@@ -2304,6 +2326,18 @@ static int ms_setup(gh_ctx* c) {
   GH_HIP(hipMemcpy(c->d_ms_lut_w, lw.data(), lb, hipMemcpyHostToDevice));
   c->ms_k = K;
   c->lut_bytes = lb;
+  return GH_OK;
+}
+// LUT width of the multi-symbol split kernels: GH_MS_K, default 10, at least maxlen.
+static uint32_t ms_lut_bits(const Canon& cn) {
+  const char* ek = getenv("GH_MS_K");
+  return (uint32_t)std::clamp(ek ? atoi(ek) : 10, (int)std::max<uint32_t>(cn.maxlen, 2), 12);
+}
+static int ms_setup(gh_ctx* c) {
+  const Canon& cn = c->canon;
+  const uint32_t K = ms_lut_bits(cn);
+  if (int rc = ms_build_luts(c, K)) return rc;
+  const size_t lb = c->lut_bytes;
   c->tb = TB_MS;
   c->super = U_MS;
   c->ntiles = (uint32_t)ceil_div(c->nseg, (uint64_t)U_MS * TB_MS);
@@ -2343,6 +2377,76 @@ static int ms_setup(gh_ctx* c) {
   GH_HIP(hipMalloc(&c->d_seg_cnt, c->nseg + 16));
   GH_HIP(hipMalloc(&c->d_wg_tot, 8ull * c->grid * c->count_per + 16));
   c->ms = true;
+  c->split = false;
+  c->tile = false;
+  return GH_OK;
+}
+
+// Wave-independent split kernels (gh_wsplit.hip): the msplit LUTs, a per-wave staging
+// buffer, ranges of `bpr` blocks of 64 * WS_U segments handed out by tickets.
+struct WsKernels {
+  const void* count;
+  const void* write;
+};
+template <int GL>
+static WsKernels ws_pair() {
+  return {(const void*)gh_ws_count_kernel<WS_U, WS_TB, GL>, (const void*)gh_ws_write_kernel<WS_U, WS_TB, GL>};
+}
+static WsKernels ws_kernels(uint32_t K) {
+  const int g = ms_group(K);
+  return g >= 4 ? ws_pair<4>() : g == 3 ? ws_pair<3>() : ws_pair<2>();
+}
+static int ws_setup(gh_ctx* c, double avg_seg_bytes) {
+  const Canon& cn = c->canon;
+  const uint32_t K = ms_lut_bits(cn);
+  if (int rc = ms_build_luts(c, K)) return rc;
+  const size_t lb = c->lut_bytes;
+  constexpr int NW = WS_TB / 64;
+  const uint32_t maxsyms = std::min<uint32_t>(143 / std::max<uint32_t>(cn.minlen, 1) + 1, 255);
+  // per-wave staging: at least one chain's worst case (64 segments x maxsyms), and a
+  // typical whole block (both chains) with room to spare when the LDS allows
+  const size_t chain_worst = 64ull * maxsyms + 64;
+  const size_t full_worst = 64ull * WS_U * maxsyms + 64;
+  const size_t typical = (size_t)(1.3 * avg_seg_bytes * 64 * WS_U) + 64;
+  const size_t want = std::max(chain_worst, std::min(full_worst, typical));
+  size_t stage = 0;
+  for (int wg = 8; wg >= 1 && stage == 0; --wg) {
+    const long avail = ((long)(163840 / wg) - (long)lb) / NW;
+    if (avail >= (long)want) stage = std::min<size_t>((size_t)avail, full_worst + 15) & ~15ull;
+  }
+  if (stage == 0) {
+    const long avail = ((long)163840 - (long)lb) / NW;
+    if (avail < (long)chain_worst) return fail(GH_E_HIP, "wsplit staging does not fit");
+    stage = (size_t)avail & ~15ull;
+  }
+  if (const char* es = getenv("GH_MS_STAGE"))  // tests: force a small staging (per-chain blocks)
+    stage = std::max<size_t>((size_t)atoll(es), (chain_worst + 15) & ~15ull) & ~15ull;
+  c->stage_bytes = (uint32_t)stage;
+  c->lds = lb + NW * stage;
+  c->lds_count = std::max<size_t>(lb, 64);
+  const WsKernels k = ws_kernels(K);
+  int pc_c = 0, pc_w = 0;
+  GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc_c, k.count, WS_TB, c->lds_count));
+  GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc_w, k.write, WS_TB, c->lds));
+  if (pc_c < 1 || pc_w < 1) return fail(GH_E_HIP, "wsplit kernels do not fit on a CU");
+  c->ws_nblocks = (uint32_t)ceil_div(c->nseg, (uint64_t)64 * WS_U);
+  const uint64_t wg_blocks = ceil_div(c->ws_nblocks, (uint64_t)NW);  // workgroups that have a block
+  c->grid = (uint32_t)std::min<uint64_t>((uint64_t)pc_w * c->num_cu, wg_blocks);
+  c->ws_grid_c = (uint32_t)std::min<uint64_t>((uint64_t)pc_c * c->num_cu, wg_blocks);
+  if (const char* eg = getenv("GH_WS_GRID")) {  // tests: few workgroups, many blocks per wave
+    c->grid = (uint32_t)std::clamp<long>(atol(eg), 1, (long)c->grid);
+    c->ws_grid_c = (uint32_t)std::clamp<long>(atol(eg), 1, (long)c->ws_grid_c);
+  }
+  c->ws_nranges = c->grid * (uint32_t)NW;  // one contiguous range per wave of the write grid
+  c->ntiles = c->ws_nblocks;
+  c->super = WS_U;
+  c->tb = WS_TB;
+  c->ms_wu = WS_U;
+  GH_HIP(hipMalloc(&c->d_seg_cnt, c->nseg + 16));
+  GH_HIP(hipMalloc(&c->d_rng_tot, 8ull * c->ws_nranges + 16));
+  GH_HIP(hipMalloc(&c->d_rng_off, 8ull * c->ws_nranges + 16));
+  c->ws = true;
+  c->ms = false;
   c->split = false;
   c->tile = false;
   return GH_OK;
@@ -2647,20 +2751,22 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
       for (uint32_t l = 1; l <= 16; ++l) kraft += (uint64_t)c->canon.count[l] << (16 - l);
       const bool eligible = kraft == 65536 && c->canon.maxlen <= 12 && c->canon.minlen >= 2 &&
                             c->nseg < (1ull << 31);
-      const bool want = envm ? !strcmp(envm, "msplit") : (!c->tables.single && c->tables.g == 0);
-        if (eligible && want) {
-        rc = ms_setup(c);
+      const bool force_ms = envm && !strcmp(envm, "msplit"), force_ws = envm && !strcmp(envm, "wsplit");
+      const bool want = envm ? (force_ms || force_ws) : (!c->tables.single && c->tables.g == 0);
+      if (eligible && want) {
+        // default: the workgroup-tile kernels (msplit) until the wave kernels measure faster
+        rc = !force_ws ? ms_setup(c) : ws_setup(c, s->g ? (double)s->n / (double)s->g : 16.0);
         if (rc) return rc;
-      } else if (envm && !strcmp(envm, "msplit")) {
+      } else if (force_ms || force_ws) {
         c->split = true;  // not eligible: the older split kernels
       }
     }
     // Grouped single-symbol split kernels (GH_MODE=gsplit): the grouped path's codes.
-    if (!c->ms && c->tables.g > 0 && c->nseg < (1ull << 31) && envm && !strcmp(envm, "gsplit")) {
+    if (!c->ms && !c->ws && c->tables.g > 0 && c->nseg < (1ull << 31) && envm && !strcmp(envm, "gsplit")) {
       rc = gs_setup(c);
       if (rc) return rc;
     }
-    if (c->split && !c->ms && !c->gs) {
+    if (c->split && !c->ms && !c->gs && !c->ws) {
       // split mode: tiles of U*256 segments, U = 2 (single-symbol) or 1/2 (multi)
       if (c->tables.single || c->tables.g > 0) uv = 2;
       else if (!(envu && atoi(envu) == 2)) uv = (2u * TB_S * c->tables.maxsyms_seg <= 16384) ? 2 : 1;
@@ -2689,8 +2795,8 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
       GH_HIP(hipMalloc(&c->d_tile_cnt, 4ull * c->ntiles + 16));
       GH_HIP(hipMalloc(&c->d_wg_tot, 8ull * c->grid * c->count_per + 16));
     }
-    if (!c->tile && !c->ms && !c->gs) c->tb = c->split ? TB_S : c->tables.g > 0 ? TB_G : TB;
-    for (; !c->split && !c->tile && !c->ms && !c->gs; uv >>= 1) {  // fall back to a narrower ILP width if the kernel does not fit
+    if (!c->tile && !c->ms && !c->gs && !c->ws) c->tb = c->split ? TB_S : c->tables.g > 0 ? TB_G : TB;
+    for (; !c->split && !c->tile && !c->ms && !c->gs && !c->ws; uv >>= 1) {  // fall back to a narrower ILP width if the kernel does not fit
       c->super = (uint32_t)uv;
       c->stage_bytes = (uint32_t)(((uint64_t)uv * c->tb * c->tables.maxsyms_seg + 64 + 15) & ~15ull);
       c->lds = lut_bytes + FB_BYTES + 2 * c->stage_bytes + SCRATCH_BYTES;
@@ -2758,7 +2864,7 @@ extern "C" int gh_ctx_load(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e
                      hipMemcpyHostToDevice));
   c->gap_nib0 = (uint32_t)(b - 8 * gw0);
   c->ms_last_end = 0;
-  if (c->ms && e == s->g) {
+  if ((c->ms || c->ws) && e == s->g) {
     uint32_t w5[5] = {};
     for (uint64_t i = 0; i < 5; ++i)
       if (4 * (e - 1) + i < s->w) std::memcpy(&w5[i], (const uint8_t*)s->payload + 4 * (4 * (e - 1) + i), 4);
@@ -2804,7 +2910,7 @@ extern "C" int gh_ctx_load_device(gh_ctx* c, const gh_stream* s, uint64_t b, uin
     c->first_start = (wv >> (4 * (nib & 7))) & 15u;
   }
   c->ms_last_end = 0;
-  if (c->ms && e == s->g) {
+  if ((c->ms || c->ws) && e == s->g) {
     uint32_t w5[5] = {};
     const uint64_t lw0 = 4 * (c->nseg - 1);  // local word of the last segment
     const uint64_t nw = std::min<uint64_t>(5, have > lw0 ? have - lw0 : 0);
@@ -2820,6 +2926,26 @@ extern "C" int gh_ctx_load_device(gh_ctx* c, const gh_stream* s, uint64_t b, uin
   }
   c->loaded = true;
   return GH_OK;
+}
+
+// Persistent kernels whose workgroups wait on each other (tile, fused) assume that the
+// whole grid is resident.  Two of them running at once on one device (several shard
+// contexts on one GPU, each on its own stream) can each hold half the CUs and wait
+// forever for the rest (their bounded spins then report GH_ST_TIMEOUT).  So launches
+// of such kernels on one device are chained: each waits for the previous one's
+// completion event, whatever stream either was launched on.
+struct DevChain {
+  std::mutex mu;
+  hipEvent_t last = nullptr;
+  bool has = false;
+};
+static DevChain& dev_chain(int device) {
+  static std::mutex mu;
+  static std::map<int, DevChain*> m;
+  std::lock_guard<std::mutex> g(mu);
+  DevChain*& d = m[device];
+  if (!d) d = new DevChain();  // one per device, for the life of the process
+  return *d;
 }
 
 extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
@@ -2906,6 +3032,39 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     const GsKernels k = gs_kernels(c->tile_g);
     GH_HIP(hipLaunchKernel(k.count, dim3(c->grid * c->count_per), dim3(TB_GS), ga, c->lds_count, st));
     GH_HIP(hipLaunchKernel(k.write, dim3(c->grid), dim3(TB_GS), ga, c->lds, st));
+  } else if (c->ws) {
+    WsParams m{};
+    m.payload = c->d_payload;
+    m.gaps = c->d_gaps;
+    m.seg_cnt = c->d_seg_cnt;
+    m.rng_tot = c->d_rng_tot;
+    m.rng_off = c->d_rng_off;
+    m.out = c->d_out;
+    m.status = c->d_misc + 1;
+    m.total = (unsigned long long*)(c->d_misc + 2);
+    m.out_cap = c->out_cap;
+    m.nseg = (uint32_t)c->nseg;
+    m.nblocks = c->ws_nblocks;
+    m.nranges = c->ws_nranges;
+    m.gap_nib0 = c->gap_nib0;
+    m.first_start = c->first_start;
+    m.kbits = c->ms_k;
+    m.lut_bytes = (uint32_t)c->lut_bytes;
+    m.stage_bytes = c->stage_bytes;
+    m.last_end = c->ms_last_end;
+    static thread_local WsParams wc, ww;
+    static thread_local void* ac[1];
+    static thread_local void* aw[1];
+    wc = m;
+    wc.lut = c->d_ms_lut_c;
+    ww = m;
+    ww.lut = c->d_ms_lut_w;
+    ac[0] = &wc;
+    aw[0] = &ww;
+    const WsKernels wk = ws_kernels(c->ms_k);
+    GH_HIP(hipLaunchKernel(wk.count, dim3(c->ws_grid_c), dim3(WS_TB), ac, c->lds_count, st));
+    GH_HIP(hipLaunchKernel((const void*)gh_ws_scan_kernel, dim3(1), dim3(WS_SCAN_TB), ac, 0, st));
+    GH_HIP(hipLaunchKernel(wk.write, dim3(c->grid), dim3(WS_TB), aw, c->lds, st));
   } else if (c->ms) {
     MsParams m{};
     m.payload = c->d_payload;
@@ -2939,6 +3098,10 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     GH_HIP(hipLaunchKernel(mk.count, dim3(c->grid * c->count_per), dim3(TB_MS), ac, c->lds_count, st));
     GH_HIP(hipLaunchKernel(mk.write, dim3(c->grid), dim3(mk.tbw), aw, c->lds, st));
   } else if (c->tile) {
+    DevChain& dc = dev_chain(c->device);
+    std::lock_guard<std::mutex> chain_lock(dc.mu);
+    if (!dc.last) GH_HIP(hipEventCreateWithFlags(&dc.last, hipEventDisableTiming));
+    if (dc.has) GH_HIP(hipStreamWaitEvent(st, dc.last, 0));
     TileParams t{};
     t.payload = c->d_payload;
     t.gaps = c->d_gaps;
@@ -2971,6 +3134,8 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     ta[0] = &tp;
     GH_HIP(hipLaunchKernel(tile_kernel_for(c->tile_path, c->tile_g), dim3(c->grid), dim3(c->tb), ta, c->lds,
                            st));
+    GH_HIP(hipEventRecord(dc.last, st));
+    dc.has = true;
   } else if (c->split) {
     const SplitKernels k = split_for(c->tables.single, c->tables.needs_fb, (int)c->super,
                                      c->tables.g);
@@ -2979,9 +3144,15 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
                            c->lds_count, st));
     GH_HIP(hipLaunchKernel(k.write, dim3(c->grid), dim3(TB_S), args_of(p), c->lds, st));
   } else {
+    DevChain& dc = dev_chain(c->device);
+    std::lock_guard<std::mutex> chain_lock(dc.mu);
+    if (!dc.last) GH_HIP(hipEventCreateWithFlags(&dc.last, hipEventDisableTiming));
+    if (dc.has) GH_HIP(hipStreamWaitEvent(st, dc.last, 0));
     GH_HIP(hipLaunchKernel(kernel_for(c->tables.single, c->tables.needs_fb, (int)c->super,
                                       c->tables.g),
                            dim3(c->grid), dim3(c->tb), args_of(p), c->lds, st));
+    GH_HIP(hipEventRecord(dc.last, st));
+    dc.has = true;
   }
   GH_HIP(hipGetLastError());
   if (timed) {
@@ -3026,11 +3197,11 @@ extern "C" int gh_ctx_report(gh_ctx* c, void* hip_stream, gh_report* rep) {
     rep->lut_bits = c->tables.K;
     rep->grid = c->grid;
     rep->tiles = c->ntiles;
-    rep->mode = c->tile ? GH_MODE_TILE : (c->split || c->ms || c->gs) ? GH_MODE_SPLIT : GH_MODE_FUSED;
+    rep->mode = c->tile ? GH_MODE_TILE : (c->split || c->ms || c->gs || c->ws) ? GH_MODE_SPLIT : GH_MODE_FUSED;
     std::memcpy(&rep->slow_lookbacks, misc + 4, 8);
-    rep->path = c->ms ? GH_PATH_MULTI_LEAN
+    rep->path = c->ws ? GH_PATH_MULTI_WAVE : c->ms ? GH_PATH_MULTI_LEAN
                 : c->tables.g > 0 ? GH_PATH_GROUPED : c->tables.single ? GH_PATH_SINGLE : GH_PATH_MULTI;
-    if (c->ms) rep->lut_bits = c->ms_k;
+    if (c->ms || c->ws) rep->lut_bits = c->ms_k;
     rep->launches = c->nlaunch;
     rep->kernel_ms = c->nlaunch ? (float)(c->acc_ms / c->nlaunch) : 0.f;
   }

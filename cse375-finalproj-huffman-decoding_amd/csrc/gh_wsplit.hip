@@ -1,0 +1,338 @@
+// Wave-independent split decode ("wsplit"), included by gh_decode.hip after
+// gh_msplit.hip (whose LUT format and per-lookup helpers it shares).
+//
+// Same code shapes as msplit (complete code, maxlen <= K <= 12, minlen >= 2: one K-bit
+// lookup yields up to four symbols), same two decode passes as the reference
+// (count, scan, decode again and write: decoder.cu:529-728), but with no workgroup
+// barrier and no inter-workgroup wait inside either decode pass.  The unit of work is
+// a wave block: U chains x 64 consecutive segments (lane l of chain u owns segment
+// 64u + l of the block).  The blocks are cut into `nranges` contiguous ranges
+// (range r = blocks [r*nb/R, (r+1)*nb/R)), one per wave of the write grid; a wave
+// of the count grid takes ranges w, w + W, ...  (An atomic ticket per block measured
+// ~0.4 ms per kernel on cfg2: one counter serves ~90 M tickets/s.  A scan over one
+// total per block was latency-bound: 363 K totals on cfg5.)
+//
+//   gh_ws_count_kernel  counts the codewords of every segment (1 byte per segment)
+//                       and each range's symbol total;
+//   gh_ws_scan_kernel   one workgroup: exclusive scan of the range totals -> the
+//                       output offset of every range, and the stream total;
+//   gh_ws_write_kernel  decodes each block again, ORs every lookup's four symbol bytes
+//                       into the wave's own LDS staging at the scanned offset, and
+//                       copies the block out with 16-byte stores aligned to the
+//                       output address, re-zeroing the staging as it reads it.
+//
+// A wave never waits for another wave: it scans its block's counts with DPP, stages
+// and copies out alone (LDS operations of one wave complete in order), and its stores
+// drain while it decodes the next block.
+//
+// Reference counterpart: the count / scan / decode passes of gpu_dec_l1_l2
+// (decoder.cu:529-728) and its decoupled look-back (:571-653), replaced here by the
+// block-total scan.
+
+constexpr int WS_TB = 256;  // threads per workgroup of the count and write kernels
+constexpr int WS_U = 2;     // chains per lane (segments per lane per block)
+constexpr int WS_SCAN_TB = 1024;
+#ifndef GH_WS_ABLATE
+#define GH_WS_ABLATE 0  // diagnostic builds only (results wrong): 1 no LDS OR, 2 no stores, 4 no copy-out
+#endif
+
+struct WsParams {
+  const uint32_t* payload;         // local segment j owns words [4j, 4j+4); +1 look-ahead, zero padded
+  const uint32_t* gaps;            // nibble gap_nib0 + j - 1: start of segment j >= 1; gap_nib0 + j: its end
+  const uint2* lut;                // count: {b, end mask}; write: {symbols, b | n << 8}; 2^K entries
+  uint8_t* seg_cnt;                // codewords per segment
+  unsigned long long* rng_tot;     // symbols per range
+  unsigned long long* rng_off;     // output offset per range (scan kernel)
+  uint8_t* out;
+  unsigned int* status;
+  unsigned long long* total;
+  unsigned long long out_cap;
+  uint32_t nseg, nblocks, nranges, gap_nib0, first_start, kbits, lut_bytes, stage_bytes;
+  uint32_t last_end;               // != 0: end of the stream's last segment (= local segment nseg-1)
+};
+
+// Words and gap words of block `blk` for this lane (loads clamped, never skipped).
+template <int U>
+__device__ __forceinline__ void ws_load(const WsParams& p, uint32_t blk, int lane, uint4 (&w)[U],
+                                        uint32_t (&w4)[U], uint32_t (&ga)[U], uint32_t (&gb)[U]) {
+  const uint32_t b = min(blk, p.nblocks - 1);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t seg = b * (uint32_t)(64 * U) + (uint32_t)(64 * u + lane);
+    const uint32_t sc = min(seg, p.nseg - 1);
+    w[u] = *(const uint4*)(p.payload + 4ull * sc);
+    w4[u] = p.payload[4ull * sc + 4];
+    ga[u] = p.gaps[(p.gap_nib0 + (sc ? sc - 1u : 0u)) >> 3];
+    gb[u] = p.gaps[(p.gap_nib0 + sc) >> 3];
+  }
+}
+
+template <int TBK>
+__device__ __forceinline__ void ws_lut_to_lds(const WsParams& p, uint8_t* smem, int tid) {
+  const uint4* g = (const uint4*)p.lut;
+  uint4* s4 = (uint4*)smem;
+  for (uint32_t i = tid; i < p.lut_bytes / 16; i += TBK) s4[i] = g[i];
+}
+
+template <int U, int TBK, int GL>
+__global__ __launch_bounds__(TBK) void gh_ws_count_kernel(const WsParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const uint32_t sh = 29u - p.kbits;  // index bits -> byte offset of a u64 entry
+  const uint32_t amask = ((1u << p.kbits) - 1u) << 3;
+  ws_lut_to_lds<TBK>(p, smem, tid);
+  if (tid == 0 && (uint32_t)(size_t)(const __attribute__((address_space(3))) uint8_t*)smem != 0u)
+    atomicOr(p.status, (unsigned)GH_ST_LAYOUT);
+  __syncthreads();
+  const uint32_t nw = gridDim.x * (uint32_t)(TBK / 64);
+  uint4 w[U];
+  uint32_t w4[U], ga[U], gb[U];
+  for (uint32_t r = blockIdx.x * (uint32_t)(TBK / 64) + (uint32_t)(tid >> 6); r < p.nranges; r += nw) {
+    const uint32_t b0 = (uint32_t)((unsigned long long)r * p.nblocks / p.nranges);
+    const uint32_t b1 = (uint32_t)((unsigned long long)(r + 1) * p.nblocks / p.nranges);
+    uint32_t tot = 0;
+    if (b0 < b1) ws_load<U>(p, b0, lane, w, w4, ga, gb);
+    for (uint32_t blk = b0; blk < b1; ++blk) {
+      Win v[U];
+      int R[U];
+      uint32_t cnt[U];
+      bool act[U];
+  #pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t seg = blk * (uint32_t)(64 * U) + (uint32_t)(64 * u + lane);
+        act[u] = seg < p.nseg;
+        const int start = seg == 0 ? (int)p.first_start : (int)ms_nib(ga[u], p.gap_nib0 + seg - 1u);
+        const int E = (p.last_end && seg == p.nseg - 1u) ? (int)p.last_end
+                                                         : 128 + (int)ms_nib(gb[u], p.gap_nib0 + seg);
+        v[u] = make_win(w[u], w4[u], start);
+        R[u] = act[u] ? E - start : 0;
+        cnt[u] = 0;
+      }
+      if (blk + 1 < b1) ws_load<U>(p, blk + 1, lane, w, w4, ga, gb);  // prefetch
+      for (int g = 0; g < 160; ++g) {
+        uint32_t rm[U], q[U];
+  #pragma unroll
+        for (int u = 0; u < U; ++u) {
+          rm[u] = ms_rmask(R[u]);
+          q[u] = 32u;
+        }
+  #pragma unroll
+        for (int j = 0; j < GL; ++j) {
+          uint2 e[U];
+  #pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const uint32_t x = j == 0 ? v[u].d0 : __builtin_amdgcn_alignbit(v[u].d0, v[u].d1, q[u]);
+            e[u] = ms_lds_u64((x >> sh) & amask);
+          }
+          ms_wait(e);
+  #pragma unroll
+          for (int u = 0; u < U; ++u) {
+            cnt[u] = __builtin_popcount(e[u].y & rm[u]) + cnt[u];
+            rm[u] = (uint32_t)((int)rm[u] >> e[u].x);
+            q[u] -= e[u].x;
+          }
+        }
+        bool more = false;
+  #pragma unroll
+        for (int u = 0; u < U; ++u) {
+          ms_shift(v[u], q[u]);
+          R[u] -= 32 - (int)q[u];
+          more |= R[u] > 0;
+        }
+        if (!__any(more)) break;
+      }
+      const unsigned long long seg0 = (unsigned long long)blk * (64 * U) + lane;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (act[u]) p.seg_cnt[seg0 + 64ull * u] = (uint8_t)cnt[u];
+        tot += act[u] ? cnt[u] : 0u;
+      }
+    }
+    unsigned long long t64 = wave_sum_u64(tot);
+    if (lane == 0) p.rng_tot[r] = t64;
+  }
+}
+
+// Exclusive scan of the range totals (one workgroup), and the stream total.
+__global__ __launch_bounds__(WS_SCAN_TB) void gh_ws_scan_kernel(const WsParams p) {
+  __shared__ unsigned long long s_w[WS_SCAN_TB / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const uint32_t per = (p.nranges + WS_SCAN_TB - 1) / WS_SCAN_TB;
+  const uint32_t i0 = min((uint32_t)tid * per, p.nranges), i1 = min(i0 + per, p.nranges);
+  unsigned long long s = 0;
+  for (uint32_t i = i0; i < i1; ++i) s += p.rng_tot[i];
+  unsigned long long incl = s;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const unsigned long long y = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += y;
+  }
+  if (lane == 63) s_w[wid] = incl;
+  __syncthreads();
+  unsigned long long base = 0, all = 0;
+#pragma unroll
+  for (int q = 0; q < WS_SCAN_TB / 64; ++q) {
+    base += q < wid ? s_w[q] : 0ull;
+    all += s_w[q];
+  }
+  unsigned long long run = base + incl - s;
+  for (uint32_t i = i0; i < i1; ++i) {
+    const unsigned long long t = p.rng_tot[i];
+    p.rng_off[i] = run;
+    run += t;
+  }
+  if (tid == 0) *p.total = all;
+}
+
+template <int U, int TBK, int GL>
+__global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
+  constexpr int NWAVE = TBK / 64;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const uint32_t sh = 29u - p.kbits;
+  const uint32_t amask = ((1u << p.kbits) - 1u) << 3;
+  ws_lut_to_lds<TBK>(p, smem, tid);
+  for (uint32_t i = tid; i < (uint32_t)NWAVE * p.stage_bytes / 16; i += TBK)
+    ((uint4*)(smem + p.lut_bytes))[i] = make_uint4(0, 0, 0, 0);
+  if (tid == 0 && (uint32_t)(size_t)(const __attribute__((address_space(3))) uint8_t*)smem != 0u)
+    atomicOr(p.status, (unsigned)GH_ST_LAYOUT);
+  __syncthreads();
+  const uint32_t stage0 = p.lut_bytes + (uint32_t)wid * p.stage_bytes;  // absolute LDS address
+  uint4* st4 = (uint4*)(smem + stage0);
+  uint4 w[U];
+  uint32_t w4[U], ga[U], gb[U], c8[U];
+  auto load_counts = [&](uint32_t blk) {
+    const uint32_t b = min(blk, p.nblocks - 1);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t seg = b * (uint32_t)(64 * U) + (uint32_t)(64 * u + lane);
+      c8[u] = p.seg_cnt[min(seg, p.nseg - 1)];
+    }
+  };
+  // one range per wave of this grid (nranges = waves of the grid)
+  const uint32_t r = blockIdx.x * (uint32_t)NWAVE + (uint32_t)wid;
+  const uint32_t b0 = r < p.nranges ? (uint32_t)((unsigned long long)r * p.nblocks / p.nranges) : 0u;
+  const uint32_t b1 = r < p.nranges ? (uint32_t)((unsigned long long)(r + 1) * p.nblocks / p.nranges) : 0u;
+  unsigned long long goff = 0;
+  if (b0 < b1) {
+    ws_load<U>(p, b0, lane, w, w4, ga, gb);
+    load_counts(b0);
+    const unsigned long long ro = p.rng_off[r];
+    goff = __builtin_amdgcn_readfirstlane((uint32_t)ro) |
+           ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(ro >> 32)) << 32);
+  }
+  for (uint32_t blk = b0; blk < b1; ++blk) {
+    {
+      int start[U];
+      uint32_t cc[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t seg = blk * (uint32_t)(64 * U) + (uint32_t)(64 * u + lane);
+        start[u] = seg == 0 ? (int)p.first_start : (int)ms_nib(ga[u], p.gap_nib0 + seg - 1u);
+        cc[u] = seg < p.nseg ? c8[u] : 0u;
+      }
+      uint4 wc[U];
+      uint32_t w4c[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        wc[u] = w[u];
+        w4c[u] = w4[u];
+      }
+      if (blk + 1 < b1) {  // prefetch the wave's next block
+        ws_load<U>(p, blk + 1, lane, w, w4, ga, gb);
+        load_counts(blk + 1);
+      }
+      // offsets inside the block: chain u's bytes follow chain u-1's
+      uint32_t bpos[U], ctot[U], coff[U], btot = 0;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t incl = wave_incl_scan(cc[u], lane);
+        bpos[u] = incl - cc[u];
+        ctot[u] = __builtin_amdgcn_readlane(incl, 63);
+        coff[u] = btot;
+        btot += ctot[u];
+      }
+      // a block that does not fit the wave's staging is staged one chain at a time
+      const uint32_t nh = btot + 64u <= p.stage_bytes ? 1u : (uint32_t)U;
+      for (uint32_t h = 0; h < nh; ++h) {
+        const uint32_t hbytes = nh == 1 ? btot : ctot[h];
+        const uint32_t lb = (uint32_t)(goff & 15);
+        // staging byte 16 + lb + i = byte i of this half: staging chunk c <-> output
+        // bytes [goff - lb - 16 + 16c, +16), aligned 16-byte copies
+        Win v[U];
+        uint32_t ptr[U], end[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const bool on = nh == 1 || (uint32_t)u == h;
+          v[u] = make_win(wc[u], w4c[u], start[u]);
+          ptr[u] = on ? stage0 + 16u + lb + (nh == 1 ? coff[u] : 0u) + bpos[u] : 0u;
+          end[u] = on ? ptr[u] + cc[u] : 0u;
+        }
+        for (int g = 0; g < 160; ++g) {
+          uint32_t q[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) q[u] = 32u;
+#pragma unroll
+          for (int j = 0; j < GL; ++j) {
+            uint2 e[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+              const uint32_t x = j == 0 ? v[u].d0 : __builtin_amdgcn_alignbit(v[u].d0, v[u].d1, q[u]);
+              e[u] = ms_lds_u64((x >> sh) & amask);
+            }
+            ms_wait(e);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+              if (!(GH_WS_ABLATE & 1) && ptr[u] < end[u]) ms_lds_or_bytes(ptr[u], e[u].x);
+              ptr[u] = ms_add_n(ptr[u], e[u].y);
+              q[u] -= e[u].y;
+            }
+          }
+          bool more = false;
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            ms_shift(v[u], q[u]);
+            more |= ptr[u] < end[u];
+          }
+          if (!__any(more)) break;
+        }
+        // copy out chunks [1, nz) (chunk 0 precedes the bytes) and zero [0, nz + 1)
+        // (the last lookup may spill past the end); this wave's LDS operations
+        // complete in order, so the reads see every OR above
+        const unsigned long long a0 = goff - lb;
+        const unsigned long long oend = min(goff + hbytes, p.out_cap);
+        const uint32_t nz = (16u + lb + hbytes + 15u) >> 4;
+        for (uint32_t c0 = lane; !(GH_WS_ABLATE & 4) && c0 < nz + 1u; c0 += 4u * 64u) {
+          uint4 d[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const uint32_t c = c0 + (uint32_t)i * 64u;
+            d[i] = c < nz + 1u ? st4[c] : make_uint4(0, 0, 0, 0);
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const uint32_t c = c0 + (uint32_t)i * 64u;
+            if (c < nz + 1u) st4[c] = make_uint4(0, 0, 0, 0);
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const uint32_t c = c0 + (uint32_t)i * 64u;
+            const unsigned long long gs = a0 - 16 + 16ull * c;
+            if (c == 0 || c >= nz + 1u || gs >= oend || (GH_WS_ABLATE & 2)) continue;
+            if (gs >= goff && gs + 16 <= oend) {
+              *(uint4*)(p.out + gs) = d[i];
+            } else {
+              const uint32_t wv[4] = {d[i].x, d[i].y, d[i].z, d[i].w};
+#pragma unroll
+              for (int k = 0; k < 16; ++k) {
+                const unsigned long long ga2 = gs + k;
+                if (ga2 >= goff && ga2 < oend) p.out[ga2] = (uint8_t)(wv[k >> 2] >> (8 * (k & 3)));
+              }
+            }
+          }
+        }
+        goff += hbytes;
+      }
+    }
+  }
+}

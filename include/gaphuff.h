@@ -161,6 +161,8 @@ typedef struct gh_report {
 #define GH_PATH_GROUPED 2u  /* single-symbol LUT, grouped window shifts              */
 #define GH_PATH_MULTI_LEAN 3u /* multi-symbol LUT (complete code, maxlen <= 12):
                                  end-mask count kernel + unaligned-store write kernel */
+#define GH_PATH_MULTI_WAVE 4u /* multi-symbol LUT, wave-independent count / scan / write
+                                 kernels (no barriers, ranges by ticket) */
 
 #define GH_ST_BADCODE 1u    /* a bit pattern outside the code space was met       */
 #define GH_ST_TIMEOUT 2u    /* look-back spin gave up (never expected)            */

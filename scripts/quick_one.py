@@ -1,10 +1,18 @@
+# One workload, one lib (GAPHUFF_LIB): 3 untimed decodes, then `reps` timed; prints the
+# average kernel time, roofline fraction and bit-exactness.
+# Usage: python scripts/quick_one.py name:N:r [reps]
 import sys, os
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', 'cse375-finalproj-huffman-decoding_amd'))
 import numpy as np, gaphuff as gh
 name, n, r = sys.argv[1].split(":"); n = int(n); r = float(r)
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 data = gh.generate(375, r, n); img = gh.encode(data); s = gh.parse(img)
+alg = 4 * s.w + 4 * ((s.g + 7) // 8) + s.n
 d = gh.Decoder(0); d.load(s)
+for _ in range(3): d.decode(timed=False)
+d.report(); d.reset_timing()
 for _ in range(reps): d.decode()
 rep = d.report()
-print(name, "kernel_ms", rep.kernel_ms, "ok", np.array_equal(d.download(s.n), data), "alg_bytes", 4*s.w + 4*((s.g+7)//8) + s.n)
+ok = bool(np.array_equal(d.download(s.n), data)) and rep.status == 0
+print(f"{name} ms={rep.kernel_ms:.4f} frac={alg / rep.kernel_ms / 1e6 / 8000:.4f} mode={gh.MODE_NAMES.get(rep.mode)} "
+      f"K={rep.lut_bits} grid={rep.grid} st={rep.status} ok={ok}", flush=True)

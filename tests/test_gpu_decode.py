@@ -224,14 +224,19 @@ def test_graft_smoke(gpu):
 
 @pytest.mark.parametrize("k", ["", "10", "11", "12"])
 @pytest.mark.parametrize("stage", ["", "1"])
-@pytest.mark.parametrize("wu", ["", "1", "2"])
+@pytest.mark.parametrize("wu", ["", "1", "2", "ws", "ws1", "ws3"])  # "wsN": GH_WS_GRID=N
 def test_lean_split_widths_and_staging(gpu, orc, k, stage, wu, monkeypatch):
-    """The lean multi-symbol split kernels (gh_msplit.hip) at every LUT width, with the
-    default staging and with the staging forced down to one chain's worst case, so
-    that tiles are staged one chain at a time (GH_MS_STAGE), and with either write
-    geometry (GH_MS_WU: one chain per thread x 512, or two x 256)."""
-    monkeypatch.setenv("GH_MODE", "msplit")
-    if wu:
+    """The multi-symbol split kernels at every LUT width, with the default staging and
+    with the staging forced down to one chain's worst case, so that blocks are staged
+    one chain at a time (GH_MS_STAGE).  wu "", "1", "2": the workgroup-tile kernels
+    (gh_msplit.hip) with either write geometry (GH_MS_WU: one chain per thread x 512,
+    or two x 256); "ws*": the wave-independent kernels (gh_wsplit.hip) on the default
+    grid and on grids of 1 and 3 workgroups (GH_WS_GRID: each wave walks many blocks)."""
+    ws = wu.startswith("ws")
+    monkeypatch.setenv("GH_MODE", "wsplit" if ws else "msplit")
+    if ws and wu[2:]:
+        monkeypatch.setenv("GH_WS_GRID", wu[2:])
+    if wu and not ws:
         monkeypatch.setenv("GH_MS_WU", wu)
     if k:
         monkeypatch.setenv("GH_MS_K", k)
@@ -246,17 +251,18 @@ def test_lean_split_widths_and_staging(gpu, orc, k, stage, wu, monkeypatch):
             d.decode()
             rep = d.report()
         if max(l for _, l in s.symbols) <= 12:
-            assert gpu.PATH_NAMES[rep.path] == "multi_lean"
+            assert gpu.PATH_NAMES[rep.path] == ("multi_wave" if ws else "multi_lean")
         total = sum(orc.segment_count(img, i) for i in range(s.g)) if n < 100_000 else None
         if total is not None:
             assert rep.symbols == total
 
 
-def test_lean_split_shard_counts(gpu, orc, monkeypatch):
-    """Shards through the lean split kernels: per-shard symbol counts equal the
+@pytest.mark.parametrize("mode", ["msplit", "wsplit"])
+def test_lean_split_shard_counts(gpu, orc, mode, monkeypatch):
+    """Shards through the multi-symbol split kernels: per-shard symbol counts equal the
     reference segment rule's (decoder.cu:529-569), including the stream's last
     segment (its zero padding, last_segment_end)."""
-    monkeypatch.setenv("GH_MODE", "msplit")
+    monkeypatch.setenv("GH_MODE", mode)
     data = gpu.generate(35, 0.5, 250_000)
     img = gpu.encode(data)
     s = gpu.parse(img)
@@ -291,3 +297,24 @@ def test_grouped_split_and_tile(gpu, orc, mode, monkeypatch):
         assert gpu.PATH_NAMES[rep.path] == "grouped" and rep.status == 0
         if n < 200_000:
             assert rep.symbols == sum(orc.segment_count(img, i) for i in range(s.g))
+
+
+@pytest.mark.parametrize("grid", ["", "1", "7"])
+def test_wave_split_repeated_and_default(gpu, orc, grid, monkeypatch):
+    """The wave-independent split kernels (GH_MODE=wsplit): back-to-back decodes
+    (timed and not) give identical bytes and totals, on the default grid and on
+    small ones (GH_WS_GRID)."""
+    monkeypatch.setenv("GH_MODE", "wsplit")
+    if grid:
+        monkeypatch.setenv("GH_WS_GRID", grid)
+    for seed, r, n in ((51, 0.5, 3_000_001), (52, 0.9, 1_234_567)):
+        data = gpu.generate(seed, r, n)
+        s = gpu.parse(gpu.encode(data))
+        with gpu.Decoder(0) as d:
+            d.load(s)
+            for i in range(4):
+                d.decode(timed=bool(i & 1))
+                rep = d.report()
+                assert gpu.PATH_NAMES[rep.path] == "multi_wave" and rep.status == 0
+                assert rep.symbols >= n
+                assert np.array_equal(d.download(n), data)
