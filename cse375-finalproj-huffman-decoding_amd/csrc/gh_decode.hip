@@ -2390,7 +2390,7 @@ struct WsKernels {
 };
 template <int GL>
 static WsKernels ws_pair() {
-  return {(const void*)gh_ws_count_kernel<WS_U, WS_TB, GL>, (const void*)gh_ws_write_kernel<WS_U, WS_TB, GL>};
+  return {(const void*)gh_ws_count_kernel<WS_UC, WS_TB, GL>, (const void*)gh_ws_write_kernel<WS_U, WS_TB, GL>};
 }
 static WsKernels ws_kernels(uint32_t K) {
   const int g = ms_group(K);
@@ -2429,8 +2429,8 @@ static int ws_setup(gh_ctx* c, double avg_seg_bytes) {
   GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc_c, k.count, WS_TB, c->lds_count));
   GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc_w, k.write, WS_TB, c->lds));
   if (pc_c < 1 || pc_w < 1) return fail(GH_E_HIP, "wsplit kernels do not fit on a CU");
-  c->ws_nblocks = (uint32_t)ceil_div(c->nseg, (uint64_t)64 * WS_U);
-  const uint64_t wg_blocks = ceil_div(c->ws_nblocks, (uint64_t)NW);  // workgroups that have a block
+  c->ws_nblocks = (uint32_t)ceil_div(c->nseg, (uint64_t)WS_SB);  // superblocks
+  const uint64_t wg_blocks = ceil_div(c->ws_nblocks, (uint64_t)NW);  // workgroups that have a superblock
   c->grid = (uint32_t)std::min<uint64_t>((uint64_t)pc_w * c->num_cu, wg_blocks);
   c->ws_grid_c = (uint32_t)std::min<uint64_t>((uint64_t)pc_c * c->num_cu, wg_blocks);
   if (const char* eg = getenv("GH_WS_GRID")) {  // tests: few workgroups, many blocks per wave
@@ -3044,7 +3044,7 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     m.total = (unsigned long long*)(c->d_misc + 2);
     m.out_cap = c->out_cap;
     m.nseg = (uint32_t)c->nseg;
-    m.nblocks = c->ws_nblocks;
+    m.nsb = c->ws_nblocks;
     m.nranges = c->ws_nranges;
     m.gap_nib0 = c->gap_nib0;
     m.first_start = c->first_start;

@@ -68,10 +68,13 @@ __device__ __forceinline__ uint2 ms_lds_u64(uint32_t a) {
 }
 template <int U>
 __device__ __forceinline__ void ms_wait(uint2 (&v)[U]) {
+  static_assert(U == 1 || U == 2 || U == 4, "ms_wait: 1, 2 or 4 lookups");
   if constexpr (U == 1) {
     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]) :: "memory");
-  } else {
+  } else if constexpr (U == 2) {
     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]) :: "memory");
+  } else {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]) :: "memory");
   }
 }
 // OR the four bytes v into LDS at byte address a (any alignment): two aligned

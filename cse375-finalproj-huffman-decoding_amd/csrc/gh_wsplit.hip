@@ -30,7 +30,12 @@
 // block-total scan.
 
 constexpr int WS_TB = 256;  // threads per workgroup of the count and write kernels
-constexpr int WS_U = 2;     // chains per lane (segments per lane per block)
+constexpr int WS_U = 2;     // chains per lane of the write kernel (segments per lane per block)
+#ifndef GH_WS_UC
+#define GH_WS_UC 4
+#endif
+constexpr int WS_UC = GH_WS_UC;  // chains per lane of the count kernel
+constexpr int WS_SB = 256;  // segments per superblock: ranges are cut at superblock edges
 constexpr int WS_SCAN_TB = 1024;
 #ifndef GH_WS_ABLATE
 #define GH_WS_ABLATE 0  // diagnostic builds only (results wrong): 1 no LDS OR, 2 no stores, 4 no copy-out
@@ -47,18 +52,29 @@ struct WsParams {
   unsigned int* status;
   unsigned long long* total;
   unsigned long long out_cap;
-  uint32_t nseg, nblocks, nranges, gap_nib0, first_start, kbits, lut_bytes, stage_bytes;
+  uint32_t nseg, nsb, nranges, gap_nib0, first_start, kbits, lut_bytes, stage_bytes;
   uint32_t last_end;               // != 0: end of the stream's last segment (= local segment nseg-1)
 };
+
+// Blocks [b0, b1) of 64*U segments of range r (ranges are cut at superblock edges, so
+// kernels with different U cover the same segments).
+template <int U>
+__device__ __forceinline__ void ws_range(const WsParams& p, uint32_t r, uint32_t& b0, uint32_t& b1) {
+  constexpr uint32_t BPS = WS_SB / (64 * U);
+  const uint32_t s0 = (uint32_t)((unsigned long long)r * p.nsb / p.nranges);
+  const uint32_t s1 = (uint32_t)((unsigned long long)(r + 1) * p.nsb / p.nranges);
+  const uint32_t nb = (p.nseg + 64 * U - 1) / (64 * U);
+  b0 = min(s0 * BPS, nb);
+  b1 = min(s1 * BPS, nb);
+}
 
 // Words and gap words of block `blk` for this lane (loads clamped, never skipped).
 template <int U>
 __device__ __forceinline__ void ws_load(const WsParams& p, uint32_t blk, int lane, uint4 (&w)[U],
                                         uint32_t (&w4)[U], uint32_t (&ga)[U], uint32_t (&gb)[U]) {
-  const uint32_t b = min(blk, p.nblocks - 1);
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    const uint32_t seg = b * (uint32_t)(64 * U) + (uint32_t)(64 * u + lane);
+    const uint32_t seg = blk * (uint32_t)(64 * U) + (uint32_t)(64 * u + lane);
     const uint32_t sc = min(seg, p.nseg - 1);
     w[u] = *(const uint4*)(p.payload + 4ull * sc);
     w4[u] = p.payload[4ull * sc + 4];
@@ -88,8 +104,8 @@ __global__ __launch_bounds__(TBK) void gh_ws_count_kernel(const WsParams p) {
   uint4 w[U];
   uint32_t w4[U], ga[U], gb[U];
   for (uint32_t r = blockIdx.x * (uint32_t)(TBK / 64) + (uint32_t)(tid >> 6); r < p.nranges; r += nw) {
-    const uint32_t b0 = (uint32_t)((unsigned long long)r * p.nblocks / p.nranges);
-    const uint32_t b1 = (uint32_t)((unsigned long long)(r + 1) * p.nblocks / p.nranges);
+    uint32_t b0, b1;
+    ws_range<U>(p, r, b0, b1);
     uint32_t tot = 0;
     if (b0 < b1) ws_load<U>(p, b0, lane, w, w4, ga, gb);
     for (uint32_t blk = b0; blk < b1; ++blk) {
@@ -202,17 +218,16 @@ __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
   uint4 w[U];
   uint32_t w4[U], ga[U], gb[U], c8[U];
   auto load_counts = [&](uint32_t blk) {
-    const uint32_t b = min(blk, p.nblocks - 1);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const uint32_t seg = b * (uint32_t)(64 * U) + (uint32_t)(64 * u + lane);
+      const uint32_t seg = blk * (uint32_t)(64 * U) + (uint32_t)(64 * u + lane);
       c8[u] = p.seg_cnt[min(seg, p.nseg - 1)];
     }
   };
   // one range per wave of this grid (nranges = waves of the grid)
   const uint32_t r = blockIdx.x * (uint32_t)NWAVE + (uint32_t)wid;
-  const uint32_t b0 = r < p.nranges ? (uint32_t)((unsigned long long)r * p.nblocks / p.nranges) : 0u;
-  const uint32_t b1 = r < p.nranges ? (uint32_t)((unsigned long long)(r + 1) * p.nblocks / p.nranges) : 0u;
+  uint32_t b0 = 0, b1 = 0;
+  if (r < p.nranges) ws_range<U>(p, r, b0, b1);
   unsigned long long goff = 0;
   if (b0 < b1) {
     ws_load<U>(p, b0, lane, w, w4, ga, gb);
