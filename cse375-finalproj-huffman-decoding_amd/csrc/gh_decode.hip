@@ -1234,6 +1234,15 @@ __global__ __launch_bounds__(TBK) void gh_write_kernel(const DecodeParams p) {
 // two VALU ops.  Reference counterpart: gpu_dec_l1_l2 (decoder.cu:454-730).
 // ============================================================================
 constexpr int STAGE_PAD = 16;  // staging byte STAGE_PAD + i = tile byte i
+#ifndef GH_TILE_WPE
+#define GH_TILE_WPE 4  // most waves per SIMD the tile kernel is compiled for (VGPR budget 512 / WPE)
+#endif
+#ifndef GH_TILE_FIXST
+#define GH_TILE_FIXST 1        // grouped path: copy-out with a fixed store count per thread, prefetch before it
+#endif
+#ifndef GH_TILE_NS
+#define GH_TILE_NS 2           // 16-byte stores per thread per copy-out (the rest of a large tile loops)
+#endif
 #ifndef GH_PREFETCH_LATE
 #define GH_PREFETCH_LATE 1     // grouped path: issue the next tile's loads after the copy-out
 #endif
@@ -1271,6 +1280,7 @@ struct TileParams {
   unsigned int stage_bytes;      // one staging buffer
   unsigned long long* stamps;    // diagnostic build only (GH_STAMPS)
   unsigned int ablate;           // diagnostic build only: 2 no copy-out, 4 no staging, 8 no decode
+  uint4* junk;                   // GH_TILE_FIXST: 16 bytes per thread of the grid for padding stores
 };
 
 // e-window of a segment starting at bit `start` (0..15): e-stream bit 0 is segment
@@ -1564,6 +1574,49 @@ __device__ __forceinline__ void copy_out_tile(uint8_t* out, uint32_t stg, unsign
   }
 }
 
+// The same copy with a fixed number of store instructions per thread: NS 16-byte
+// stores (interior chunks, or the thread's junk slot) and one byte store (a byte of
+// the two partial edge chunks, or junk).  On gfx950 loads and stores share one
+// in-order counter (vmcnt); with a fixed store count after the next tile's prefetch
+// loads, the compiler waits for those loads with vmcnt(NS + 1) instead of vmcnt(0),
+// so a wave no longer waits for its previous copy-out's stores to be acknowledged.
+template <int TBK, int NS>
+__device__ __forceinline__ void copy_out_tile_fixed(uint8_t* out, uint32_t stg, unsigned long long goff, uint32_t n,
+                                                    int tid, uint4* junk) {
+  const uint32_t lb = (uint32_t)(goff & 15);
+  uint8_t* o = out + (goff - lb);          // 16-byte aligned
+  const uint32_t src = stg + 16u - lb;     // staging address of output chunk 0
+  const uint32_t cf = lb ? 1u : 0u;        // interior chunks [cf, ce)
+  const uint32_t ce = n ? (lb + n) >> 4 : 0u;
+#pragma unroll
+  for (int i = 0; i < NS; ++i) {
+    const uint32_t c = cf + (uint32_t)tid + (uint32_t)(TBK * i);
+    const bool real = c < ce;
+    const uint4 v = lds_u128(src + 16u * (real ? c : cf));
+    *(real ? (uint4*)(o + 16ull * c) : junk) = v;
+  }
+  for (uint32_t c = cf + (uint32_t)tid + (uint32_t)(TBK * NS); c < ce; c += TBK)
+    *(uint4*)(o + 16ull * c) = lds_u128(src + 16u * c);
+  // edge bytes: the head chunk's [lb, min(16, lb + n)) when lb != 0, then the tail
+  // chunk's [0, (lb + n) & 15) when it is another chunk; one byte per thread
+  const uint32_t nh = (lb && n) ? min(16u, lb + n) - lb : 0u;
+  const uint32_t tl = (lb + n) & 15u;
+  const uint32_t nt = (n && tl && (ce > 0 || !lb)) ? tl : 0u;
+  const uint32_t t = (uint32_t)tid;
+  uint32_t k = 0;                          // output byte offset from o
+  bool real = false;
+  if (t < nh) {
+    k = lb + t;
+    real = true;
+  } else if (t < nh + nt) {
+    k = 16u * ce + (t - nh);
+    real = true;
+  }
+  uint32_t b;
+  asm volatile("ds_read_u8 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(b) : "v"(src + (real ? k : 0u)) : "memory");
+  *(real ? o + k : (uint8_t*)junk) = (uint8_t)b;
+}
+
 // ---- prefixes by round leaders ------------------------------------------------
 // Tiles are processed in rounds: workgroup b takes tile rG + b in iteration r
 // (static round robin over the G resident workgroups).  A tile publishes its
@@ -1607,7 +1660,7 @@ __device__ __forceinline__ bool granule_ok(const TileParams& p, unsigned long lo
 // TB threads, U segments per lane, PATH (TP_*), GRP codewords per window shift
 // (grouped path).
 template <int TB, int U, int PATH, int GRP>
-__global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4)))
+__global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, GH_TILE_WPE)))
 void gh_tile_kernel(const TileParams p) {
   constexpr int NWAVE_T = TB / 64;
   constexpr int LDR_NB = TB / 64;  // leader batches: one wave per 64 * LPL tiles of a round
@@ -1674,6 +1727,7 @@ void gh_tile_kernel(const TileParams p) {
   // its prefix); multi path: staged at once (emit pass), copied out at lag 2.
   constexpr bool LAG3 = GH_TILE_LAG3 && !MULTI;
   constexpr bool TOP = LAG3 && GH_TILE_TOPCOPY;  // copy-out before the decode (prefix two iterations old)
+  constexpr bool FIXST = GH_TILE_FIXST && !MULTI && !TOP;  // fixed-count copy-out, prefetch just before it
   uint32_t t1 = NONE, t2 = NONE, t3 = NONE;  // tiles of iterations k-1, k-2, k-3
   uint32_t tot1 = 0, tot2 = 0, tot3 = 0;     // their totals
   uint32_t buf = 0;               // k & 1
@@ -1749,8 +1803,17 @@ void gh_tile_kernel(const TileParams p) {
       STAMP(6);
       const uint32_t n2 =
           goff >= p.out_cap ? 0u : (uint32_t)min<unsigned long long>(LAG3 ? tot3 : tot2, p.out_cap - goff);
-      if (!ABLATE(2)) copy_out_tile<TB>(p.out, p.lut_bytes + (LAG3 ? buf ^ 1u : buf) * p.stage_bytes, goff, n2, tid,
-                                      (uint32_t)ABLATE(0xFFFFFFFFu));
+      if constexpr (FIXST) {
+        load(nxt);  // the next tile's words, issued before this copy-out's stores
+        if (!ABLATE(2))
+          copy_out_tile_fixed<TB, GH_TILE_NS>(p.out, p.lut_bytes + (LAG3 ? buf ^ 1u : buf) * p.stage_bytes, goff, n2,
+                                              tid, p.junk + (unsigned long long)blockIdx.x * TB + tid);
+      } else if (!ABLATE(2)) {
+        copy_out_tile<TB>(p.out, p.lut_bytes + (LAG3 ? buf ^ 1u : buf) * p.stage_bytes, goff, n2, tid,
+                          (uint32_t)ABLATE(0xFFFFFFFFu));
+      }
+    } else if constexpr (FIXST) {
+      load(nxt);
     }
     };
     if constexpr (TOP) {
@@ -1798,7 +1861,7 @@ void gh_tile_kernel(const TileParams p) {
         start[u] = seg == 0 ? (int)p.first_start : (int)((gw[u] >> (4 * nib)) & 15u);
         make_ewin(w[u], w4[u], start[u], S, e[u]);
       }
-      if constexpr (TOP || !GH_PREFETCH_LATE) load(nxt);  // prefetch the next iteration's tile
+      if constexpr (!FIXST && (TOP || !GH_PREFETCH_LATE)) load(nxt);  // prefetch the next iteration's tile
       if (have_cur && ABLATE(8)) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -1822,7 +1885,7 @@ void gh_tile_kernel(const TileParams p) {
     STAMP(0);
     if constexpr (!TOP) copy_block();
     STAMP(1);
-    if constexpr (!MULTI && !TOP && GH_PREFETCH_LATE) load(nxt);  // prefetch the next tile after the copy-out's waits
+    if constexpr (!MULTI && !TOP && !FIXST && GH_PREFETCH_LATE) load(nxt);  // prefetch the next tile after the copy-out's waits
     uint32_t bpos[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -2185,6 +2248,9 @@ struct gh_ctx {
   bool gs = false;         // grouped single-symbol split kernels (gh_gsplit.hip)
   bool ws = false;         // wave-independent split kernels (gh_wsplit.hip)
   uint32_t ws_nblocks = 0, ws_nranges = 0, ws_grid_c = 0;
+  int ws_ns = 4;
+  uint4* d_ws_junk = nullptr;
+  uint4* d_tile_junk = nullptr;  // tile mode: one 16-byte slot per thread of the grid
   unsigned long long* d_rng_tot = nullptr;
   unsigned long long* d_rng_off = nullptr;
   uint32_t ms_k = 0;       // their LUT width
@@ -2248,6 +2314,10 @@ static void free_shard(gh_ctx* c) {
   (void)hipFree(c->d_ms_lut_w);
   (void)hipFree(c->d_rng_tot);
   (void)hipFree(c->d_rng_off);
+  (void)hipFree(c->d_ws_junk);
+  c->d_ws_junk = nullptr;
+  (void)hipFree(c->d_tile_junk);
+  c->d_tile_junk = nullptr;
   c->d_rng_tot = nullptr;
   c->d_rng_off = nullptr;
   c->ws = false;
@@ -2388,13 +2458,24 @@ struct WsKernels {
   const void* count;
   const void* write;
 };
-template <int GL>
+template <int GL, int NS>
 static WsKernels ws_pair() {
-  return {(const void*)gh_ws_count_kernel<WS_UC, WS_TB, GL>, (const void*)gh_ws_write_kernel<WS_U, WS_TB, GL>};
+  return {(const void*)gh_ws_count_kernel<WS_UC, WS_TB, GL>, (const void*)gh_ws_write_kernel<WS_U, WS_TB, GL, NS>};
 }
-static WsKernels ws_kernels(uint32_t K) {
+template <int GL>
+static WsKernels ws_pair_ns(int ns) {
+  return ns <= 2 ? ws_pair<GL, 2>() : ns <= 3 ? ws_pair<GL, 3>() : ns <= 4 ? ws_pair<GL, 4>()
+         : ns <= 6 ? ws_pair<GL, 6>() : ws_pair<GL, 8>();
+}
+// NS (store instructions per lane per piece): the typical piece's 16-byte chunks / 64
+static WsKernels ws_kernels(uint32_t K, int ns) {
   const int g = ms_group(K);
-  return g >= 4 ? ws_pair<4>() : g == 3 ? ws_pair<3>() : ws_pair<2>();
+  return g >= 4 ? ws_pair_ns<4>(ns) : g == 3 ? ws_pair_ns<3>(ns) : ws_pair_ns<2>(ns);
+}
+static int ws_ns_for(double avg_seg_bytes) {
+  const double chunks = avg_seg_bytes * 64 * WS_U / 16.0 * 1.15 + 2;
+  const int ns = (int)std::ceil(chunks / 64);
+  return ns <= 2 ? 2 : ns <= 3 ? 3 : ns <= 4 ? 4 : ns <= 6 ? 6 : 8;
 }
 static int ws_setup(gh_ctx* c, double avg_seg_bytes) {
   const Canon& cn = c->canon;
@@ -2424,7 +2505,9 @@ static int ws_setup(gh_ctx* c, double avg_seg_bytes) {
   c->stage_bytes = (uint32_t)stage;
   c->lds = lb + NW * stage;
   c->lds_count = std::max<size_t>(lb, 64);
-  const WsKernels k = ws_kernels(K);
+  c->ws_ns = ws_ns_for(avg_seg_bytes);
+  if (const char* en = getenv("GH_WS_NS")) c->ws_ns = std::clamp(atoi(en), 2, 8);
+  const WsKernels k = ws_kernels(K, c->ws_ns);
   int pc_c = 0, pc_w = 0;
   GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc_c, k.count, WS_TB, c->lds_count));
   GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc_w, k.write, WS_TB, c->lds));
@@ -2443,6 +2526,7 @@ static int ws_setup(gh_ctx* c, double avg_seg_bytes) {
   c->tb = WS_TB;
   c->ms_wu = WS_U;
   GH_HIP(hipMalloc(&c->d_seg_cnt, c->nseg + 16));
+  GH_HIP(hipMalloc(&c->d_ws_junk, 16ull * 64 * c->ws_nranges));
   GH_HIP(hipMalloc(&c->d_rng_tot, 8ull * c->ws_nranges + 16));
   GH_HIP(hipMalloc(&c->d_rng_off, 8ull * c->ws_nranges + 16));
   c->ws = true;
@@ -2736,6 +2820,7 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
       if (per_cu >= 1) {
         // a round's aggregates are read by its leader, LPL per lane: grid <= LPL * TB
         const uint64_t gmax = (uint64_t)TB * (TB >= 512 ? 1 : 1024 / TB);
+        if (const char* ep = getenv("GH_TILE_PERCU")) per_cu = std::clamp(atoi(ep), 1, per_cu);  // diagnostics
         c->grid = (uint32_t)std::min<uint64_t>({(uint64_t)c->ntiles, (uint64_t)per_cu * c->num_cu, gmax});
       } else {  // e.g. 1-2 bit codes: the staging does not fit; use the split kernels
         c->tile = false;
@@ -2812,6 +2897,7 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
       if (uv == 1) break;
     }
     if (c->grid == 0) return fail(GH_E_HIP, "decode kernel does not fit on a CU");
+    if (c->tile) GH_HIP(hipMalloc(&c->d_tile_junk, 16ull * c->grid * c->tb));
 #ifdef GH_STAMPS
     GH_HIP(hipMalloc(&c->d_stamps, 16ull * 8 * c->grid));
     GH_HIP(hipMemset(c->d_stamps, 0, 16ull * 8 * c->grid));
@@ -3040,6 +3126,7 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     m.rng_tot = c->d_rng_tot;
     m.rng_off = c->d_rng_off;
     m.out = c->d_out;
+    m.junk = c->d_ws_junk;
     m.status = c->d_misc + 1;
     m.total = (unsigned long long*)(c->d_misc + 2);
     m.out_cap = c->out_cap;
@@ -3061,7 +3148,7 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     ww.lut = c->d_ms_lut_w;
     ac[0] = &wc;
     aw[0] = &ww;
-    const WsKernels wk = ws_kernels(c->ms_k);
+    const WsKernels wk = ws_kernels(c->ms_k, c->ws_ns);
     GH_HIP(hipLaunchKernel(wk.count, dim3(c->ws_grid_c), dim3(WS_TB), ac, c->lds_count, st));
     GH_HIP(hipLaunchKernel((const void*)gh_ws_scan_kernel, dim3(1), dim3(WS_SCAN_TB), ac, 0, st));
     GH_HIP(hipLaunchKernel(wk.write, dim3(c->grid), dim3(WS_TB), aw, c->lds, st));
@@ -3128,6 +3215,7 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     t.stage_bytes = c->stage_bytes;
     t.stamps = c->d_stamps;
     t.ablate = p.ablate;
+    t.junk = c->d_tile_junk;
     static thread_local void* ta[1];
     static thread_local TileParams tp;
     tp = t;

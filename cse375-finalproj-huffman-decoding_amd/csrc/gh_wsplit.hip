@@ -29,7 +29,10 @@
 // (decoder.cu:529-728) and its decoupled look-back (:571-653), replaced here by the
 // block-total scan.
 
-constexpr int WS_TB = 256;  // threads per workgroup of the count and write kernels
+#ifndef GH_WS_TB
+#define GH_WS_TB 256
+#endif
+constexpr int WS_TB = GH_WS_TB;  // threads per workgroup of the count and write kernels
 constexpr int WS_U = 2;     // chains per lane of the write kernel (segments per lane per block)
 #ifndef GH_WS_UC
 #define GH_WS_UC 4
@@ -49,6 +52,7 @@ struct WsParams {
   unsigned long long* rng_tot;     // symbols per range
   unsigned long long* rng_off;     // output offset per range (scan kernel)
   uint8_t* out;
+  uint4* junk;                     // write kernel: 64 16-byte slots per wave for padding stores
   unsigned int* status;
   unsigned long long* total;
   unsigned long long out_cap;
@@ -124,7 +128,7 @@ __global__ __launch_bounds__(TBK) void gh_ws_count_kernel(const WsParams p) {
         R[u] = act[u] ? E - start : 0;
         cnt[u] = 0;
       }
-      if (blk + 1 < b1) ws_load<U>(p, blk + 1, lane, w, w4, ga, gb);  // prefetch
+      ws_load<U>(p, min(blk + 1, b1 - 1), lane, w, w4, ga, gb);  // prefetch (always: fixed load count)
       for (int g = 0; g < 160; ++g) {
         uint32_t rm[U], q[U];
   #pragma unroll
@@ -200,7 +204,19 @@ __global__ __launch_bounds__(WS_SCAN_TB) void gh_ws_scan_kernel(const WsParams p
   if (tid == 0) *p.total = all;
 }
 
-template <int U, int TBK, int GL>
+// Byte-exact store of staging chunk bytes [k0, k1) of one 16-byte chunk (lanes 0..15).
+__device__ __forceinline__ void ws_store_bytes(uint8_t* dst, const uint4* chunk, uint32_t k0, uint32_t k1, int lane) {
+  if (lane < 16 && (uint32_t)lane >= k0 && (uint32_t)lane < k1) {
+    const uint8_t* b = (const uint8_t*)chunk;
+    dst[lane] = b[lane];
+  }
+}
+
+// NS: global store instructions per lane per staged piece (fixed, so the compiler can
+// wait for the prefetched loads with vmcnt(NS + ...) instead of vmcnt(0): on gfx950
+// loads and stores share one in-order counter, and a vmcnt(0) at the top of every block
+// made each wave wait for its previous block's stores to be acknowledged).
+template <int U, int TBK, int GL, int NS>
 __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
   constexpr int NWAVE = TBK / 64;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -236,6 +252,13 @@ __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
     goff = __builtin_amdgcn_readfirstlane((uint32_t)ro) |
            ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(ro >> 32)) << 32);
   }
+  // Staging chunk 1 holds the output chunk containing goff.  Its bytes before goff
+  // come from the previous piece of this range (carried), except at the range's start
+  // where the first hs bytes belong to the previous range: that chunk is stored
+  // byte-exact once, as is the range's last, partial chunk.
+  uint32_t hs = (uint32_t)(goff & 15);
+  const unsigned long long rs = goff;  // the range's first output byte
+  uint4* junk = p.junk + ((unsigned long long)(blockIdx.x * (uint32_t)NWAVE + (uint32_t)wid) * 64u + lane);
   for (uint32_t blk = b0; blk < b1; ++blk) {
     {
       int start[U];
@@ -253,9 +276,10 @@ __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
         wc[u] = w[u];
         w4c[u] = w4[u];
       }
-      if (blk + 1 < b1) {  // prefetch the wave's next block
-        ws_load<U>(p, blk + 1, lane, w, w4, ga, gb);
-        load_counts(blk + 1);
+      {  // prefetch the wave's next block (always issued: a fixed count of loads)
+        const uint32_t nb = min(blk + 1, b1 - 1);
+        ws_load<U>(p, nb, lane, w, w4, ga, gb);
+        load_counts(nb);
       }
       // offsets inside the block: chain u's bytes follow chain u-1's
       uint32_t bpos[U], ctot[U], coff[U], btot = 0;
@@ -311,43 +335,47 @@ __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
           }
           if (!__any(more)) break;
         }
-        // copy out chunks [1, nz) (chunk 0 precedes the bytes) and zero [0, nz + 1)
-        // (the last lookup may spill past the end); this wave's LDS operations
-        // complete in order, so the reads see every OR above
+        // Copy out the complete chunks [c_lo, cend) of this piece: staging chunk c <->
+        // output bytes [goff - lb - 16 + 16c, +16) (the OR-s above are complete: this
+        // wave's LDS operations run in order).  Exactly NS store instructions per lane,
+        // padded with stores to the wave's junk slots; more chunks than 64 * NS (never
+        // with the host's staging sizes) go through a loop of its own.
         const unsigned long long a0 = goff - lb;
-        const unsigned long long oend = min(goff + hbytes, p.out_cap);
-        const uint32_t nz = (16u + lb + hbytes + 15u) >> 4;
-        for (uint32_t c0 = lane; !(GH_WS_ABLATE & 4) && c0 < nz + 1u; c0 += 4u * 64u) {
-          uint4 d[4];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const uint32_t c = c0 + (uint32_t)i * 64u;
-            d[i] = c < nz + 1u ? st4[c] : make_uint4(0, 0, 0, 0);
-          }
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const uint32_t c = c0 + (uint32_t)i * 64u;
-            if (c < nz + 1u) st4[c] = make_uint4(0, 0, 0, 0);
-          }
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const uint32_t c = c0 + (uint32_t)i * 64u;
-            const unsigned long long gs = a0 - 16 + 16ull * c;
-            if (c == 0 || c >= nz + 1u || gs >= oend || (GH_WS_ABLATE & 2)) continue;
-            if (gs >= goff && gs + 16 <= oend) {
-              *(uint4*)(p.out + gs) = d[i];
-            } else {
-              const uint32_t wv[4] = {d[i].x, d[i].y, d[i].z, d[i].w};
-#pragma unroll
-              for (int k = 0; k < 16; ++k) {
-                const unsigned long long ga2 = gs + k;
-                if (ga2 >= goff && ga2 < oend) p.out[ga2] = (uint8_t)(wv[k >> 2] >> (8 * (k & 3)));
-              }
-            }
-          }
+        const uint32_t hb = goff + hbytes <= p.out_cap ? hbytes : (goff < p.out_cap ? (uint32_t)(p.out_cap - goff) : 0u);
+        const uint32_t cend = ((lb + hb) >> 4) + 1u;  // chunks [1, cend) end inside the piece
+        uint32_t c_lo = 1;
+        if (hs != 0 && cend > 1u) {  // the range's first chunk is complete: its bytes [hs, 16)
+          if (!(GH_WS_ABLATE & 2)) ws_store_bytes(p.out + a0, st4 + 1, hs, 16u, lane);
+          c_lo = 2;
+          hs = 0;
         }
+        if (!(GH_WS_ABLATE & 4)) {
+#pragma unroll
+          for (int i = 0; i < NS; ++i) {
+            const uint32_t c = c_lo + (uint32_t)lane + 64u * (uint32_t)i;
+            const bool real = c < cend;
+            const uint4 d = st4[real ? c : 0u];
+            uint4* dst = real ? (uint4*)(p.out + a0 - 16 + 16ull * c) : junk;
+            if (!(GH_WS_ABLATE & 2)) *dst = d;
+          }
+          for (uint32_t c = c_lo + (uint32_t)lane + 64u * NS; c < cend; c += 64u)
+            if (!(GH_WS_ABLATE & 2)) *(uint4*)(p.out + a0 - 16 + 16ull * c) = st4[c];
+        }
+        // carry the partial chunk cend to chunk 1 (the next piece's first output chunk;
+        // bytes past the piece's end are that piece's first symbols, decoded here by the
+        // last lookups, the same values it ORs in) and zero the rest, spill included
+        const uint4 carry = st4[cend];
+        const uint32_t nzero = cend + 2u;
+        for (uint32_t c = lane; c < nzero; c += 64u) st4[c] = make_uint4(0, 0, 0, 0);
+        if (lane == 0) st4[1] = carry;
         goff += hbytes;
       }
     }
+  }
+  // the range's last, partial chunk: its bytes [hs or 0, end & 15), end clamped at out_cap
+  if (b0 < b1) {
+    const unsigned long long ge = min(goff, p.out_cap);
+    const uint32_t te = (uint32_t)(ge & 15);
+    if (te != 0 && ge > rs && !(GH_WS_ABLATE & 2)) ws_store_bytes(p.out + (ge - te), st4 + 1, hs, te, lane);
   }
 }

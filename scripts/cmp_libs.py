@@ -8,6 +8,10 @@ for wl in sys.argv[1].split(","):
     for name in sys.argv[2:]:
         lib = os.path.join(libdir, f"libgaphuff{'' if name == 'base' else '_' + name}.so")
         env = dict(os.environ, GAPHUFF_LIB=lib)
-        r = subprocess.run([sys.executable, os.path.join(here, "quick_one.py"), wl, "20"], env=env,
-                           capture_output=True, text=True, timeout=300)
+        try:
+            r = subprocess.run([sys.executable, os.path.join(here, "quick_one.py"), wl, "20"], env=env,
+                           capture_output=True, text=True, timeout=90)
+        except subprocess.TimeoutExpired:
+            print(f"{name:10s} TIMEOUT (90 s)", flush=True)
+            break
         print(f"{name:10s} {r.stdout.strip()} {r.stderr.strip()[-300:] if r.returncode else ''}", flush=True)

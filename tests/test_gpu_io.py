@@ -89,29 +89,46 @@ def test_gpu_cli_streaming_verify(gpu, tmp_path, gpus, shards):
     assert np.array_equal(np.fromfile(out, dtype=np.uint8), d)
 
 
+_CALLER_STREAM_SCRIPT = r"""
+import sys, numpy as np, torch
+torch.cuda.init()  # torch's HIP runtime first (as bench.py does), then the library's
+sys.path.insert(0, sys.argv[1])
+import gaphuff as gh
+path, out, n = sys.argv[2], sys.argv[3], int(sys.argv[4])
+d = np.fromfile(sys.argv[5], dtype=np.uint8)
+s = torch.cuda.Stream()
+with gh.Decoder(0) as dec:
+    dec.load_file(path)
+    for _ in range(3):
+        dec.decode(s.cuda_stream, timed=True)
+    dec.save_file(out, n)  # no caller sync before this
+    assert np.array_equal(np.fromfile(out, dtype=np.uint8), d)
+    dec.decode(s.cuda_stream, timed=True)
+    assert np.array_equal(dec.download(n), d)
+    dec.decode(s.cuda_stream, timed=True)
+    t = torch.empty(n, dtype=torch.uint8, device="cuda")
+    dec.copy_output(t.data_ptr(), n)  # context stream, ordered after the decode
+    rep = dec.report()
+    assert rep.status == 0 and rep.launches == 5, (rep.status, rep.launches)
+    assert np.array_equal(t.cpu().numpy(), d)
+print("caller-stream ok")
+"""
+
+
 @pytest.mark.gpu
 def test_decode_on_caller_stream_then_save_and_download(gpu, tmp_path):
     """A decode launched on a caller's stream (as bench.py does with torch's stream) is
     waited for by save_file / download / copy_output on the context's own stream
-    (gh_ctx completion event), with no synchronisation by the caller."""
-    import torch
+    (gh_ctx completion event), with no synchronisation by the caller.  Runs in a child
+    process that initialises torch before the library, as bench.py does."""
+    import sys
     d, path = _write(tmp_path, gpu, 8, 0.1, 30_000_001)
-    s = torch.cuda.Stream()
-    with gpu.Decoder(0) as dec:
-        dec.load_file(path)
-        for _ in range(3):
-            dec.decode(s.cuda_stream, timed=True)
-        out = str(tmp_path / "o.bin")
-        dec.save_file(out, d.size)  # no caller sync before this
-        assert np.array_equal(np.fromfile(out, dtype=np.uint8), d)
-        dec.decode(s.cuda_stream, timed=True)
-        assert np.array_equal(dec.download(d.size), d)
-        dec.decode(s.cuda_stream, timed=True)
-        t = torch.empty(d.size, dtype=torch.uint8, device="cuda")
-        dec.copy_output(t.data_ptr(), d.size)  # context stream, ordered after the decode
-        rep = dec.report()
-        assert rep.status == 0 and rep.launches == 5
-        assert np.array_equal(t.cpu().numpy(), d)
+    orig = tmp_path / "orig.bin"
+    d.tofile(orig)
+    r = subprocess.run([sys.executable, "-c", _CALLER_STREAM_SCRIPT, os.path.join(ROOT, "cse375-finalproj-huffman-decoding_amd"),
+                        path, str(tmp_path / "o.bin"), str(d.size), str(orig)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "caller-stream ok" in r.stdout, r.stdout[-1000:] + r.stderr[-2000:]
 
 
 @pytest.mark.gpu
