@@ -2839,8 +2839,8 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
       const bool force_ms = envm && !strcmp(envm, "msplit"), force_ws = envm && !strcmp(envm, "wsplit");
       const bool want = envm ? (force_ms || force_ws) : (!c->tables.single && c->tables.g == 0);
       if (eligible && want) {
-        // default: the workgroup-tile kernels (msplit) until the wave kernels measure faster
-        rc = !force_ws ? ms_setup(c) : ws_setup(c, s->g ? (double)s->n / (double)s->g : 16.0);
+        // default: the wave-independent kernels (measured faster than msplit on cfg2/3/5)
+        rc = force_ms ? ms_setup(c) : ws_setup(c, s->g ? (double)s->n / (double)s->g : 16.0);
         if (rc) return rc;
       } else if (force_ms || force_ws) {
         c->split = true;  // not eligible: the older split kernels
