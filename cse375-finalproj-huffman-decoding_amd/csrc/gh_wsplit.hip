@@ -16,10 +16,10 @@
 //                       and each range's symbol total;
 //   gh_ws_scan_kernel   one workgroup: exclusive scan of the range totals -> the
 //                       output offset of every range, and the stream total;
-//   gh_ws_write_kernel  decodes each block again, gathers every lookup's symbol bytes
-//                       in a per-segment accumulator written to the wave's own LDS
-//                       staging 4 bytes at a time at the scanned offset, and copies the
-//                       block out with 16-byte stores aligned to the output address.
+//   gh_ws_write_kernel  decodes each block again, ORs every lookup's four symbol bytes
+//                       into the wave's own LDS staging at the scanned offset, and
+//                       copies the block out with 16-byte stores aligned to the
+//                       output address, re-zeroing the staging as it reads it.
 //
 // A wave never waits for another wave: it scans its block's counts with DPP, stages
 // and copies out alone (LDS operations of one wave complete in order), and its stores
@@ -299,31 +299,14 @@ __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
         // staging byte 16 + lb + i = byte i of this half: staging chunk c <-> output
         // bytes [goff - lb - 16 + 16c, +16), aligned 16-byte copies
         Win v[U];
-        // Each lookup's symbol bytes go into a per-chain 64-bit accumulator; every 4
-        // bytes become one ds_write_b32 at the segment's running position (the first
-        // one possibly unaligned, the rest aligned), the last 0-3 bytes b16/b8
-        // writes.  Every byte of the piece is written exactly once by its owner (bytes
-        // past a segment's end that its last lookup decoded are the next segment's
-        // first symbols: the same values), so the staging needs no zeroing.
-        uint32_t wpos[U], fill[U];
-        int rem[U];
-        uint64_t acc[U];
+        uint32_t ptr[U], end[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const bool on = nh == 1 || (uint32_t)u == h;
           v[u] = make_win(wc[u], w4c[u], start[u]);
-          wpos[u] = stage0 + 16u + lb + (nh == 1 ? coff[u] : 0u) + bpos[u];
-          rem[u] = on ? (int)cc[u] : 0;
-          fill[u] = 0;
-          acc[u] = 0;
+          ptr[u] = on ? stage0 + 16u + lb + (nh == 1 ? coff[u] : 0u) + bpos[u] : 0u;
+          end[u] = on ? ptr[u] + cc[u] : 0u;
         }
-        auto flush = [&](int u) {
-          if (!(GH_WS_ABLATE & 1)) asm volatile("ds_write_b32 %0, %1" :: "v"(wpos[u]), "v"((uint32_t)acc[u]) : "memory");
-          const uint32_t adv = 4u - (wpos[u] & 3u);  // 4 once aligned
-          acc[u] >>= 8u * adv;
-          fill[u] -= adv;
-          wpos[u] += adv;
-        };
         for (int g = 0; g < 160; ++g) {
           uint32_t q[U];
 #pragma unroll
@@ -339,14 +322,8 @@ __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
             ms_wait(e);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-              if (rem[u] > 0) {
-                const uint32_t n = (e[u].y >> 8) & 7u;
-                acc[u] |= (uint64_t)e[u].x << (8u * fill[u]);
-                fill[u] += n;
-                rem[u] -= (int)n;
-                if (fill[u] >= 4u) flush(u);
-                if (fill[u] >= 4u) flush(u);  // only after an unaligned first write
-              }
+              if (!(GH_WS_ABLATE & 1) && ptr[u] < end[u]) ms_lds_or_bytes(ptr[u], e[u].x);
+              ptr[u] = ms_add_n(ptr[u], e[u].y);
               q[u] -= e[u].y;
             }
           }
@@ -354,17 +331,9 @@ __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
 #pragma unroll
           for (int u = 0; u < U; ++u) {
             ms_shift(v[u], q[u]);
-            more |= rem[u] > 0;
+            more |= ptr[u] < end[u];
           }
           if (!__any(more)) break;
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {  // the last 0-3 bytes of each segment (spill included)
-          const uint32_t t = fill[u];
-          if (!(GH_WS_ABLATE & 1) && (t & 2u))
-            asm volatile("ds_write_b16 %0, %1" :: "v"(wpos[u]), "v"((uint32_t)acc[u]) : "memory");
-          if (!(GH_WS_ABLATE & 1) && (t & 1u))
-            asm volatile("ds_write_b8 %0, %1" :: "v"(wpos[u] + (t & 2u)), "v"((uint32_t)(acc[u] >> (8u * (t & 2u)))) : "memory");
         }
         // Copy out the complete chunks [c_lo, cend) of this piece: staging chunk c <->
         // output bytes [goff - lb - 16 + 16c, +16) (the OR-s above are complete: this
@@ -392,9 +361,12 @@ __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
           for (uint32_t c = c_lo + (uint32_t)lane + 64u * NS; c < cend; c += 64u)
             if (!(GH_WS_ABLATE & 2)) *(uint4*)(p.out + a0 - 16 + 16ull * c) = st4[c];
         }
-        // carry the partial chunk cend to chunk 1: the next piece's first output chunk,
-        // whose bytes from the piece's end on that piece writes itself
+        // carry the partial chunk cend to chunk 1 (the next piece's first output chunk;
+        // bytes past the piece's end are that piece's first symbols, decoded here by the
+        // last lookups, the same values it ORs in) and zero the rest, spill included
         const uint4 carry = st4[cend];
+        const uint32_t nzero = cend + 2u;
+        for (uint32_t c = lane; c < nzero; c += 64u) st4[c] = make_uint4(0, 0, 0, 0);
         if (lane == 0) st4[1] = carry;
         goff += hbytes;
       }
