@@ -64,7 +64,6 @@ WORKLOADS = {
 KERNEL_NAMES = {
     (1, 4): "gh::gh_ws_count_kernel + gh::gh_ws_scan_kernel + gh::gh_ws_write_kernel",
     (1, 3): "gh::gh_ms_count_kernel + gh::gh_ms_write_kernel",
-    (1, 2): "gh::gh_gs_count_kernel + gh::gh_gs_write_kernel",
     (1, -1): "gh::gh_count_kernel + gh::gh_write_kernel",
     (2, -1): "gh::gh_tile_kernel",
     (0, -1): "gh::gh_decode_kernel",

@@ -2016,7 +2016,6 @@ void gh_tile_kernel(const TileParams p) {
 
 #include "gh_msplit.hip"
 #include "gh_wsplit.hip"
-#include "gh_gsplit.hip"
 
 // ============================================================================
 // Host side
@@ -2245,7 +2244,6 @@ struct gh_ctx {
   uint32_t* d_lut_t = nullptr;  // tile mode: compact u32 LUT
   bool split = true;       // split mode (count / scan / write) vs the fused persistent kernel
   bool ms = false;         // lean multi-symbol split kernels (gh_msplit.hip)
-  bool gs = false;         // grouped single-symbol split kernels (gh_gsplit.hip)
   bool ws = false;         // wave-independent split kernels (gh_wsplit.hip)
   uint32_t ws_nblocks = 0, ws_nranges = 0, ws_grid_c = 0;
   int ws_ns = 4;
@@ -2324,7 +2322,6 @@ static void free_shard(gh_ctx* c) {
   c->d_ms_lut_c = nullptr;
   c->d_ms_lut_w = nullptr;
   c->ms = false;
-  c->gs = false;
   c->d_lut_t = nullptr;
   c->d_wg_tot = nullptr;
   c->d_seg_cnt = nullptr;
@@ -2531,62 +2528,6 @@ static int ws_setup(gh_ctx* c, double avg_seg_bytes) {
   GH_HIP(hipMalloc(&c->d_rng_off, 8ull * c->ws_nranges + 16));
   c->ws = true;
   c->ms = false;
-  c->split = false;
-  c->tile = false;
-  return GH_OK;
-}
-
-struct GsKernels {
-  const void* count;
-  const void* write;
-};
-template <int G>
-static GsKernels gs_pair() {
-  return {(const void*)gh_gs_count_kernel<U_GS, TB_GS, G>, (const void*)gh_gs_write_kernel<U_GS, TB_GS, G>};
-}
-static GsKernels gs_kernels(uint32_t g) { return g >= 4 ? gs_pair<4>() : g == 3 ? gs_pair<3>() : gs_pair<2>(); }
-
-// Grouped single-symbol split kernels (gh_gsplit.hip): compact LUT {len | sym << 24}
-// replicated 2^lgr times in LDS (the largest replication, up to 8, that keeps the
-// write kernel's best occupancy), one staging buffer for U_GS * TB_GS segments.
-static int gs_setup(gh_ctx* c) {
-  const uint32_t K = c->tables.K;
-  std::vector<uint32_t> lt(1u << K);
-  for (uint32_t i = 0; i < (1u << K); ++i) lt[i] = c->tables.lut2[i].x | c->tables.lut2[i].y;
-  GH_HIP(hipMalloc(&c->d_lut_t, 4ull << K));
-  GH_HIP(hipMemcpy(c->d_lut_t, lt.data(), 4ull << K, hipMemcpyHostToDevice));
-  c->tile_g = std::min<uint32_t>(4, 32 / std::max<uint32_t>(c->canon.maxlen, 1));
-  c->tb = TB_GS;
-  c->super = U_GS;
-  c->ntiles = (uint32_t)ceil_div(c->nseg, (uint64_t)U_GS * TB_GS);
-  c->stage_bytes = (uint32_t)((16 + 16 + (uint64_t)U_GS * TB_GS * c->tables.maxsyms_seg + 64 + 15) & ~15ull);
-  constexpr int NW = TB_GS / 64;
-  const size_t misc = 4 * (U_GS * NW + 2) + 8 * NW;
-  const GsKernels k = gs_kernels(c->tile_g);
-  const char* envr = getenv("GH_LGR");
-  int best = 0, best_lg = 0;
-  for (int lg = envr ? std::clamp(atoi(envr), 0, 5) : 3; lg >= 0; --lg) {
-    if ((4ull << (K + lg)) < 16) continue;
-    int pc = 0;
-    GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, k.write, TB_GS, (4ull << (K + lg)) + c->stage_bytes + misc));
-    if (pc > best) { best = pc; best_lg = lg; }
-    if (envr) break;
-  }
-  if (best < 1) return fail(GH_E_HIP, "gsplit write kernel does not fit on a CU");
-  c->lgr = (uint32_t)best_lg;
-  c->lut_bytes = 4ull << (K + best_lg);
-  c->lds = c->lut_bytes + c->stage_bytes + misc;
-  c->lds_count = std::max<size_t>(c->lut_bytes, 64);
-  int pc_c = 0;
-  GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc_c, k.count, TB_GS, c->lds_count));
-  if (pc_c < 1) return fail(GH_E_HIP, "gsplit count kernel does not fit on a CU");
-  c->grid = (uint32_t)std::min<uint64_t>(c->ntiles, (uint64_t)best * c->num_cu);
-  const uint32_t kk = std::max(1, pc_c / best);
-  c->count_per = 1;
-  for (uint32_t k2 = kk; k2 >= 1; --k2)
-    if ((uint64_t)k2 * c->grid <= c->ntiles) { c->count_per = k2; break; }
-  GH_HIP(hipMalloc(&c->d_wg_tot, 8ull * c->grid * c->count_per + 16));
-  c->gs = true;
   c->split = false;
   c->tile = false;
   return GH_OK;
@@ -2846,12 +2787,7 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
         c->split = true;  // not eligible: the older split kernels
       }
     }
-    // Grouped single-symbol split kernels (GH_MODE=gsplit): the grouped path's codes.
-    if (!c->ms && !c->ws && c->tables.g > 0 && c->nseg < (1ull << 31) && envm && !strcmp(envm, "gsplit")) {
-      rc = gs_setup(c);
-      if (rc) return rc;
-    }
-    if (c->split && !c->ms && !c->gs && !c->ws) {
+    if (c->split && !c->ms && !c->ws) {
       // split mode: tiles of U*256 segments, U = 2 (single-symbol) or 1/2 (multi)
       if (c->tables.single || c->tables.g > 0) uv = 2;
       else if (!(envu && atoi(envu) == 2)) uv = (2u * TB_S * c->tables.maxsyms_seg <= 16384) ? 2 : 1;
@@ -2880,8 +2816,8 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
       GH_HIP(hipMalloc(&c->d_tile_cnt, 4ull * c->ntiles + 16));
       GH_HIP(hipMalloc(&c->d_wg_tot, 8ull * c->grid * c->count_per + 16));
     }
-    if (!c->tile && !c->ms && !c->gs && !c->ws) c->tb = c->split ? TB_S : c->tables.g > 0 ? TB_G : TB;
-    for (; !c->split && !c->tile && !c->ms && !c->gs && !c->ws; uv >>= 1) {  // fall back to a narrower ILP width if the kernel does not fit
+    if (!c->tile && !c->ms && !c->ws) c->tb = c->split ? TB_S : c->tables.g > 0 ? TB_G : TB;
+    for (; !c->split && !c->tile && !c->ms && !c->ws; uv >>= 1) {  // fall back to a narrower ILP width if the kernel does not fit
       c->super = (uint32_t)uv;
       c->stage_bytes = (uint32_t)(((uint64_t)uv * c->tb * c->tables.maxsyms_seg + 64 + 15) & ~15ull);
       c->lds = lut_bytes + FB_BYTES + 2 * c->stage_bytes + SCRATCH_BYTES;
@@ -3092,33 +3028,7 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
   p.tile_cnt = c->d_tile_cnt;
   p.tile_off = c->d_tile_off;
   p.wg_tot = c->d_wg_tot;
-  if (c->gs) {
-    GsParams g{};
-    g.payload = c->d_payload;
-    g.gaps = c->d_gaps;
-    g.lut = c->d_lut_t;
-    g.wg_tot = c->d_wg_tot;
-    g.out = c->d_out;
-    g.status = c->d_misc + 1;
-    g.total = (unsigned long long*)(c->d_misc + 2);
-    g.out_cap = c->out_cap;
-    g.nseg = (uint32_t)c->nseg;
-    g.ntiles = c->ntiles;
-    g.gap_nib0 = c->gap_nib0;
-    g.first_start = c->first_start;
-    g.kbits = c->tables.K;
-    g.lgr = c->lgr;
-    g.lut_bytes = (uint32_t)c->lut_bytes;
-    g.stage_bytes = c->stage_bytes;
-    g.count_per = c->count_per;
-    static thread_local GsParams gp;
-    static thread_local void* ga[1];
-    gp = g;
-    ga[0] = &gp;
-    const GsKernels k = gs_kernels(c->tile_g);
-    GH_HIP(hipLaunchKernel(k.count, dim3(c->grid * c->count_per), dim3(TB_GS), ga, c->lds_count, st));
-    GH_HIP(hipLaunchKernel(k.write, dim3(c->grid), dim3(TB_GS), ga, c->lds, st));
-  } else if (c->ws) {
+  if (c->ws) {
     WsParams m{};
     m.payload = c->d_payload;
     m.gaps = c->d_gaps;
@@ -3285,7 +3195,7 @@ extern "C" int gh_ctx_report(gh_ctx* c, void* hip_stream, gh_report* rep) {
     rep->lut_bits = c->tables.K;
     rep->grid = c->grid;
     rep->tiles = c->ntiles;
-    rep->mode = c->tile ? GH_MODE_TILE : (c->split || c->ms || c->gs || c->ws) ? GH_MODE_SPLIT : GH_MODE_FUSED;
+    rep->mode = c->tile ? GH_MODE_TILE : (c->split || c->ms || c->ws) ? GH_MODE_SPLIT : GH_MODE_FUSED;
     std::memcpy(&rep->slow_lookbacks, misc + 4, 8);
     rep->path = c->ws ? GH_PATH_MULTI_WAVE : c->ms ? GH_PATH_MULTI_LEAN
                 : c->tables.g > 0 ? GH_PATH_GROUPED : c->tables.single ? GH_PATH_SINGLE : GH_PATH_MULTI;

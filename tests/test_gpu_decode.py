@@ -280,11 +280,11 @@ def test_lean_split_shard_counts(gpu, orc, mode, monkeypatch):
             off += r.symbols
 
 
-@pytest.mark.parametrize("mode", ["gsplit", "tile"])
+@pytest.mark.parametrize("mode", ["tile"])
 def test_grouped_split_and_tile(gpu, orc, mode, monkeypatch):
-    """The grouped single-symbol codes (complete, minlen >= 4) through the tile kernel
-    and through the sync-free count/write kernels (gh_gsplit.hip): bytes and symbol
-    totals equal the oracle's (reference segment rule, decoder.cu:529-569)."""
+    """The grouped single-symbol codes (complete, minlen >= 4) through the tile kernel:
+    bytes and symbol totals equal the oracle's (reference segment rule,
+    decoder.cu:529-569)."""
     monkeypatch.setenv("GH_MODE", mode)
     for seed, n in ((41, 1_000_003), (42, 131_072), (43, 9_999)):
         data = gpu.generate(seed, 0.1, n)
