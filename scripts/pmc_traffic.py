@@ -34,9 +34,10 @@ for arg in sys.argv[2:]:
         "fetch_size_kib_per_decode": fetch,
         "write_size_kib_per_decode": write,
         "kernels": sorted(per["FETCH_SIZE"]),
-        "source": f"profiles/{os.path.basename(fdir.rstrip('/'))}+{os.path.basename(wdir.rstrip('/'))}: "
+        "source": f"{fdir.rstrip('/')}+{os.path.basename(wdir.rstrip('/'))}: "
                   "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of "
-                  f"`python3 bench.py --workload {wl} --cpu-sample 0`; bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024 "
+                  f"`python3 bench.py --workload {wl.split('_')[0]} --cpu-sample 0 --no-copy`; "
+                  "bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024 "
                   "per decode, summed over its kernels (gfx950 FETCH_SIZE halves wide streaming reads)",
     }
 json.dump(res, open(out_path, "w"), indent=1)

@@ -1,48 +1,35 @@
 #!/bin/bash
-# Round GPU evidence on one MI355X: GPU tests, smoke(), bench lines (cfg2 default with
-# the CPU baseline, cfg3/cfg4 without), rocprofv3 kernel-trace stats of each bench
-# command, separate FETCH_SIZE / WRITE_SIZE PMC passes of each, and the per-decode
-# HBM traffic derived from them (gpurun_out/$R/pmc_traffic.json); then the GPU encoder's
-# numbers (scripts/bench_encode.py) and its rocprofv3 stats on cfg4.
-# Usage (from the repo root, on the box): R=r01 bash scripts/round_gpu.sh
+# Round GPU evidence on one MI355X (R=r02 bash scripts/round_gpu.sh): GPU tests (fast
+# and slow), smoke(), the default bench line (cfg4, with the CPU baselines), cfg3 / cfg2
+# / cfg5 lines, rocprofv3 kernel-trace stats of each bench command, separate
+# FETCH_SIZE / WRITE_SIZE PMC passes for cfg4 and cfg3 (-> pmc_traffic.json, keyed
+# workload_bytes_nGPUs), the GPU encoder and self-sync numbers.
 set -o pipefail
-R=${R:-r01}
+source scripts/gpu_step.sh
+R=${R:-r02}
 O=gpurun_out/$R
 mkdir -p $O
 export TMPDIR=/tmp
-step() { echo "== $1 $(date +%T)"; }
-step pytest
-timeout -k 10 900 python -m pytest tests -m "gpu and not slow" -x -q --timeout=180 > $O/pytest_gpu.log 2>&1 \
-  || { tail -40 $O/pytest_gpu.log; exit 1; }
-tail -3 $O/pytest_gpu.log
-step smoke
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { cat $O/smoke.log; exit 1; }
-cat $O/smoke.log
-step bench-cfg2
-timeout -k 10 600 python bench.py > $O/bench_cfg2.json 2> $O/bench_cfg2.err || { tail $O/bench_cfg2.err; exit 1; }
-cat $O/bench_cfg2.json
-for w in cfg3 cfg4; do
-  step bench-$w
-  timeout -k 10 600 python bench.py --workload $w --cpu-sample 0 > $O/bench_$w.json 2> $O/bench_$w.err \
-    || { tail $O/bench_$w.err; exit 1; }
-  cat $O/bench_$w.json
+step pytest 900 $O/pytest_gpu.log python -u -m pytest tests -m "gpu and not slow" -q -rf --timeout 180 --timeout-method thread
+tail -4 $O/pytest_gpu.log
+step pytest-slow 900 $O/pytest_slow.log python -u -m pytest tests -m "gpu and slow" -v -rf --timeout 600 --timeout-method thread --durations=0
+tail -12 $O/pytest_slow.log
+step smoke 300 $O/smoke.log python -c "import __graft_entry__ as g; g.smoke()"; cat $O/smoke.log
+step bench-cfg4 600 $O/bench_cfg4.err python bench.py --out-json $O/bench_cfg4.json; cat $O/bench_cfg4.json
+for w in cfg3 cfg2 cfg5; do
+  step bench-$w 400 $O/bench_$w.err python bench.py --workload $w --cpu-sample 0 --out-json $O/bench_$w.json; cat $O/bench_$w.json
 done
 TR=""
-for w in cfg2 cfg3 cfg4; do
-  step rocprof-stats-$w
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$w -o run \
-    -- python3 bench.py --workload $w --cpu-sample 0 > $O/prof_$w.log 2>&1 || { tail $O/prof_$w.log; exit 1; }
+for w in cfg4 cfg3 cfg2; do
+  step rocprof-$w 400 $O/prof_$w.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$w -o run -- python3 bench.py --workload $w --cpu-sample 0 --no-copy
+done
+for w in cfg4 cfg3; do
   for c in FETCH_SIZE WRITE_SIZE; do
-    step pmc-$c-$w
-    timeout -k 10 600 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $O/pmc_${c}_$w -o run \
-      -- python3 bench.py --workload $w --cpu-sample 0 > $O/pmc_${c}_$w.log 2>&1 || { tail $O/pmc_${c}_$w.log; exit 1; }
+    step pmc-$c-$w 300 $O/pmc_${c}_$w.log rocprofv3 --pmc $c --kernel-trace --output-format csv -d $O/pmc_${c}_$w -o run -- python3 bench.py --workload $w --cpu-sample 0 --no-copy
   done
-  TR="$TR $w=$O/pmc_FETCH_SIZE_$w,$O/pmc_WRITE_SIZE_$w"
+  TR="$TR ${w}_1000000000_n1=$O/pmc_FETCH_SIZE_$w,$O/pmc_WRITE_SIZE_$w"
 done
 python3 scripts/pmc_traffic.py $O/pmc_traffic.json $TR > /dev/null && cat $O/pmc_traffic.json
-step encoder
-timeout -k 10 300 python scripts/bench_encode.py > $O/encode.jsonl 2> $O/encode.err || { tail $O/encode.err; exit 1; }
-cat $O/encode.jsonl
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_encode -o run \
-  -- python3 scripts/bench_encode.py cfg4 > $O/prof_encode.log 2>&1 || { tail $O/prof_encode.log; exit 1; }
-step done
+step encoder 300 $O/encode.jsonl python scripts/bench_encode.py; cat $O/encode.jsonl
+step sync 300 $O/sync.jsonl python scripts/bench_sync.py; cat $O/sync.jsonl
+echo done
