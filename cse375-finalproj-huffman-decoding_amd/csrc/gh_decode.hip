@@ -320,6 +320,15 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
   return v;
 }
 
+// Wave-uniform copy of a 64-bit value (lane 0's).  readfirstlane returns int: each half
+// is taken as uint32_t before widening (an int low half with bit 31 set would
+// sign-extend over the high half).
+__device__ __forceinline__ unsigned long long rfl_u64(unsigned long long v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+  return ((unsigned long long)hi << 32) | lo;
+}
+
 // Look-back granule: [37:0] value, [39:38] flag (1 aggregate, 2 inclusive prefix),
 // [63:40] epoch of the launch that wrote it.
 __device__ __forceinline__ unsigned long long granule(unsigned epoch, unsigned flag,
@@ -1798,8 +1807,7 @@ void gh_tile_kernel(const TileParams p) {
         goff = (gp & VMASK) + (r2 > 0 ? (gr & VMASK) : 0ull);
         if (wid == 0 && tx == p.ntiles - 1) *p.total = goff + (LAG3 ? tot3 : tot2);
       }
-      goff = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(goff >> 32)) << 32) |
-             __builtin_amdgcn_readfirstlane((uint32_t)goff);
+      goff = rfl_u64(goff);
       STAMP(6);
       const uint32_t n2 =
           goff >= p.out_cap ? 0u : (uint32_t)min<unsigned long long>(LAG3 ? tot3 : tot2, p.out_cap - goff);
@@ -3043,6 +3051,9 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     m.nseg = (uint32_t)c->nseg;
     m.nsb = c->ws_nblocks;
     m.nranges = c->ws_nranges;
+    m.chk_pay = 4 * c->nseg + 16;
+    m.chk_gap = c->nseg / 8 + 4;  // (at least; the allocation holds gwords + 4)
+    m.chk_out = std::max<uint64_t>(c->out_cap, 16) + 64;
     m.gap_nib0 = c->gap_nib0;
     m.first_start = c->first_start;
     m.kbits = c->ms_k;

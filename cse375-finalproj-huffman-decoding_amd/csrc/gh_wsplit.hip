@@ -58,7 +58,16 @@ struct WsParams {
   unsigned long long out_cap;
   uint32_t nseg, nsb, nranges, gap_nib0, first_start, kbits, lut_bytes, stage_bytes;
   uint32_t last_end;               // != 0: end of the stream's last segment (= local segment nseg-1)
+  unsigned long long chk_pay, chk_gap, chk_out;  // GH_WS_CHECK builds: allocation sizes (words, words, bytes)
 };
+#ifndef GH_WS_CHECK
+#define GH_WS_CHECK 0  // diagnostic builds: bounds-check every global access, flag status bits instead
+#endif
+#if GH_WS_CHECK
+#define WS_CK(cond, bit) (((cond)) ? true : (atomicOr(p.status, (unsigned)(bit)), false))
+#else
+#define WS_CK(cond, bit) true
+#endif
 
 // Blocks [b0, b1) of 64*U segments of range r (ranges are cut at superblock edges, so
 // kernels with different U cover the same segments).
@@ -80,10 +89,14 @@ __device__ __forceinline__ void ws_load(const WsParams& p, uint32_t blk, int lan
   for (int u = 0; u < U; ++u) {
     const uint32_t seg = blk * (uint32_t)(64 * U) + (uint32_t)(64 * u + lane);
     const uint32_t sc = min(seg, p.nseg - 1);
-    w[u] = *(const uint4*)(p.payload + 4ull * sc);
-    w4[u] = p.payload[4ull * sc + 4];
-    ga[u] = p.gaps[(p.gap_nib0 + (sc ? sc - 1u : 0u)) >> 3];
-    gb[u] = p.gaps[(p.gap_nib0 + sc) >> 3];
+    if (WS_CK(4ull * sc + 5 <= p.chk_pay || !GH_WS_CHECK, 0x100)) {
+      w[u] = *(const uint4*)(p.payload + 4ull * sc);
+      w4[u] = p.payload[4ull * sc + 4];
+    }
+    if (WS_CK(((p.gap_nib0 + sc) >> 3) < p.chk_gap || !GH_WS_CHECK, 0x200)) {
+      ga[u] = p.gaps[(p.gap_nib0 + (sc ? sc - 1u : 0u)) >> 3];
+      gb[u] = p.gaps[(p.gap_nib0 + sc) >> 3];
+    }
   }
 }
 
@@ -164,12 +177,12 @@ __global__ __launch_bounds__(TBK) void gh_ws_count_kernel(const WsParams p) {
       const unsigned long long seg0 = (unsigned long long)blk * (64 * U) + lane;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        if (act[u]) p.seg_cnt[seg0 + 64ull * u] = (uint8_t)cnt[u];
+        if (act[u] && WS_CK(seg0 + 64ull * u < p.nseg, 0x400)) p.seg_cnt[seg0 + 64ull * u] = (uint8_t)cnt[u];
         tot += act[u] ? cnt[u] : 0u;
       }
     }
     unsigned long long t64 = wave_sum_u64(tot);
-    if (lane == 0) p.rng_tot[r] = t64;
+    if (lane == 0 && WS_CK(r < p.nranges, 0x800)) p.rng_tot[r] = t64;
   }
 }
 
@@ -237,7 +250,7 @@ __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t seg = blk * (uint32_t)(64 * U) + (uint32_t)(64 * u + lane);
-      c8[u] = p.seg_cnt[min(seg, p.nseg - 1)];
+      c8[u] = WS_CK(min(seg, p.nseg - 1) < p.nseg, 0x10000) ? p.seg_cnt[min(seg, p.nseg - 1)] : 0u;
     }
   };
   // one range per wave of this grid (nranges = waves of the grid)
@@ -248,9 +261,8 @@ __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
   if (b0 < b1) {
     ws_load<U>(p, b0, lane, w, w4, ga, gb);
     load_counts(b0);
-    const unsigned long long ro = p.rng_off[r];
-    goff = __builtin_amdgcn_readfirstlane((uint32_t)ro) |
-           ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(ro >> 32)) << 32);
+    const unsigned long long ro = WS_CK(r < p.nranges, 0x20000) ? p.rng_off[r] : 0ull;
+    goff = rfl_u64(ro);
   }
   // Staging chunk 1 holds the output chunk containing goff.  Its bytes before goff
   // come from the previous piece of this range (carried), except at the range's start
@@ -345,7 +357,8 @@ __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
         const uint32_t cend = ((lb + hb) >> 4) + 1u;  // chunks [1, cend) end inside the piece
         uint32_t c_lo = 1;
         if (hs != 0 && cend > 1u) {  // the range's first chunk is complete: its bytes [hs, 16)
-          if (!(GH_WS_ABLATE & 2)) ws_store_bytes(p.out + a0, st4 + 1, hs, 16u, lane);
+          if (!(GH_WS_ABLATE & 2) && WS_CK(a0 + 16 <= p.chk_out || !GH_WS_CHECK, 0x1000))
+            ws_store_bytes(p.out + a0, st4 + 1, hs, 16u, lane);
           c_lo = 2;
           hs = 0;
         }
@@ -356,10 +369,11 @@ __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
             const bool real = c < cend;
             const uint4 d = st4[real ? c : 0u];
             uint4* dst = real ? (uint4*)(p.out + a0 - 16 + 16ull * c) : junk;
-            if (!(GH_WS_ABLATE & 2)) *dst = d;
+            if (!(GH_WS_ABLATE & 2) && WS_CK(!real || a0 + 16ull * c <= p.chk_out || !GH_WS_CHECK, 0x2000)) *dst = d;
           }
           for (uint32_t c = c_lo + (uint32_t)lane + 64u * NS; c < cend; c += 64u)
-            if (!(GH_WS_ABLATE & 2)) *(uint4*)(p.out + a0 - 16 + 16ull * c) = st4[c];
+            if (!(GH_WS_ABLATE & 2) && WS_CK(a0 + 16ull * c <= p.chk_out || !GH_WS_CHECK, 0x4000))
+              *(uint4*)(p.out + a0 - 16 + 16ull * c) = st4[c];
         }
         // carry the partial chunk cend to chunk 1 (the next piece's first output chunk;
         // bytes past the piece's end are that piece's first symbols, decoded here by the
@@ -376,6 +390,7 @@ __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
   if (b0 < b1) {
     const unsigned long long ge = min(goff, p.out_cap);
     const uint32_t te = (uint32_t)(ge & 15);
-    if (te != 0 && ge > rs && !(GH_WS_ABLATE & 2)) ws_store_bytes(p.out + (ge - te), st4 + 1, hs, te, lane);
+    if (te != 0 && ge > rs && !(GH_WS_ABLATE & 2) && WS_CK(ge <= p.chk_out || !GH_WS_CHECK, 0x8000))
+      ws_store_bytes(p.out + (ge - te), st4 + 1, hs, te, lane);
   }
 }
