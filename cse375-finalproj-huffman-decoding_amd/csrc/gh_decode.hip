@@ -1584,8 +1584,9 @@ __device__ __forceinline__ void copy_out_tile(uint8_t* out, uint32_t stg, unsign
 }
 
 // The same copy with a fixed number of store instructions per thread: NS 16-byte
-// stores (interior chunks, or the thread's junk slot) and one byte store (a byte of
-// the two partial edge chunks, or junk).  On gfx950 loads and stores share one
+// stores (interior chunks; spare threads store the last interior chunk again, the
+// same bytes) and one byte store (a byte of the two partial edge chunks, or the first
+// edge byte again); the thread's junk slot only when there is nothing to duplicate.  On gfx950 loads and stores share one
 // in-order counter (vmcnt); with a fixed store count after the next tile's prefetch
 // loads, the compiler waits for those loads with vmcnt(NS + 1) instead of vmcnt(0),
 // so a wave no longer waits for its previous copy-out's stores to be acknowledged.
@@ -1597,12 +1598,14 @@ __device__ __forceinline__ void copy_out_tile_fixed(uint8_t* out, uint32_t stg, 
   const uint32_t src = stg + 16u - lb;     // staging address of output chunk 0
   const uint32_t cf = lb ? 1u : 0u;        // interior chunks [cf, ce)
   const uint32_t ce = n ? (lb + n) >> 4 : 0u;
+  const bool have = ce > cf;  // padding stores duplicate a real chunk / byte (merged in L2); junk when none
 #pragma unroll
   for (int i = 0; i < NS; ++i) {
     const uint32_t c = cf + (uint32_t)tid + (uint32_t)(TBK * i);
     const bool real = c < ce;
-    const uint4 v = lds_u128(src + 16u * (real ? c : cf));
-    *(real ? (uint4*)(o + 16ull * c) : junk) = v;
+    const uint32_t cs = real ? c : ce - 1u;  // padding: the last interior chunk again (same bytes)
+    const uint4 v = lds_u128(src + 16u * ((real || have) ? cs : cf));
+    *((real || have) ? (uint4*)(o + 16ull * cs) : junk) = v;
   }
   for (uint32_t c = cf + (uint32_t)tid + (uint32_t)(TBK * NS); c < ce; c += TBK)
     *(uint4*)(o + 16ull * c) = lds_u128(src + 16u * c);
@@ -1612,7 +1615,8 @@ __device__ __forceinline__ void copy_out_tile_fixed(uint8_t* out, uint32_t stg, 
   const uint32_t tl = (lb + n) & 15u;
   const uint32_t nt = (n && tl && (ce > 0 || !lb)) ? tl : 0u;
   const uint32_t t = (uint32_t)tid;
-  uint32_t k = 0;                          // output byte offset from o
+  const bool hb = nh + nt > 0;
+  uint32_t k = nh ? lb : 16u * ce;         // output byte offset from o (padding: the first edge byte)
   bool real = false;
   if (t < nh) {
     k = lb + t;
@@ -1622,8 +1626,8 @@ __device__ __forceinline__ void copy_out_tile_fixed(uint8_t* out, uint32_t stg, 
     real = true;
   }
   uint32_t b;
-  asm volatile("ds_read_u8 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(b) : "v"(src + (real ? k : 0u)) : "memory");
-  *(real ? o + k : (uint8_t*)junk) = (uint8_t)b;
+  asm volatile("ds_read_u8 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(b) : "v"(src + ((real || hb) ? k : 0u)) : "memory");
+  *((real || hb) ? o + k : (uint8_t*)junk) = (uint8_t)b;
 }
 
 // ---- prefixes by round leaders ------------------------------------------------

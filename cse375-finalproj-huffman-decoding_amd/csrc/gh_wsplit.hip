@@ -350,8 +350,8 @@ __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
         // Copy out the complete chunks [c_lo, cend) of this piece: staging chunk c <->
         // output bytes [goff - lb - 16 + 16c, +16) (the OR-s above are complete: this
         // wave's LDS operations run in order).  Exactly NS store instructions per lane,
-        // padded with stores to the wave's junk slots; more chunks than 64 * NS (never
-        // with the host's staging sizes) go through a loop of its own.
+        // padded with duplicate stores; more chunks than 64 * NS (never with the host's
+        // staging sizes) go through a loop of its own.
         const unsigned long long a0 = goff - lb;
         const uint32_t hb = goff + hbytes <= p.out_cap ? hbytes : (goff < p.out_cap ? (uint32_t)(p.out_cap - goff) : 0u);
         const uint32_t cend = ((lb + hb) >> 4) + 1u;  // chunks [1, cend) end inside the piece
@@ -363,12 +363,18 @@ __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
           hs = 0;
         }
         if (!(GH_WS_ABLATE & 4)) {
+          // padding stores rewrite the piece's last complete chunk (same bytes: the
+          // duplicate merges in L2 instead of costing an HBM write); the junk slot only
+          // when the piece has no complete chunk
+          const bool have = cend > c_lo;
+          const uint32_t cdup = have ? cend - 1u : 0u;
 #pragma unroll
           for (int i = 0; i < NS; ++i) {
             const uint32_t c = c_lo + (uint32_t)lane + 64u * (uint32_t)i;
             const bool real = c < cend;
-            const uint4 d = st4[real ? c : 0u];
-            uint4* dst = real ? (uint4*)(p.out + a0 - 16 + 16ull * c) : junk;
+            const uint32_t cs = real ? c : cdup;
+            const uint4 d = st4[cs];
+            uint4* dst = (real || have) ? (uint4*)(p.out + a0 - 16 + 16ull * cs) : junk;
             if (!(GH_WS_ABLATE & 2) && WS_CK(!real || a0 + 16ull * c <= p.chk_out || !GH_WS_CHECK, 0x2000)) *dst = d;
           }
           for (uint32_t c = c_lo + (uint32_t)lane + 64u * NS; c < cend; c += 64u)
