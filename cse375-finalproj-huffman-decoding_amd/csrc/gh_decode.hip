@@ -2259,6 +2259,8 @@ struct gh_ctx {
   bool ws = false;         // wave-independent split kernels (gh_wsplit.hip)
   uint32_t ws_nblocks = 0, ws_nranges = 0, ws_grid_c = 0;
   int ws_ns = 4;
+  uint32_t ws_kc = 0;              // width of the wave-split count LUT
+  uint32_t* d_ws_lut_c = nullptr;  // its u32 entries {b | end mask << 16}
   uint4* d_ws_junk = nullptr;
   uint4* d_tile_junk = nullptr;  // tile mode: one 16-byte slot per thread of the grid
   unsigned long long* d_rng_tot = nullptr;
@@ -2326,6 +2328,8 @@ static void free_shard(gh_ctx* c) {
   (void)hipFree(c->d_rng_off);
   (void)hipFree(c->d_ws_junk);
   c->d_ws_junk = nullptr;
+  (void)hipFree(c->d_ws_lut_c);
+  c->d_ws_lut_c = nullptr;
   (void)hipFree(c->d_tile_junk);
   c->d_tile_junk = nullptr;
   c->d_rng_tot = nullptr;
@@ -2467,19 +2471,64 @@ struct WsKernels {
   const void* count;
   const void* write;
 };
-template <int GL, int NS>
-static WsKernels ws_pair() {
-  return {(const void*)gh_ws_count_kernel<WS_UC, WS_TB, GL>, (const void*)gh_ws_write_kernel<WS_U, WS_TB, GL, NS>};
-}
 template <int GL>
-static WsKernels ws_pair_ns(int ns) {
-  return ns <= 2 ? ws_pair<GL, 2>() : ns <= 3 ? ws_pair<GL, 3>() : ns <= 4 ? ws_pair<GL, 4>()
-         : ns <= 6 ? ws_pair<GL, 6>() : ws_pair<GL, 8>();
+static const void* ws_write_ns(int ns) {
+  return ns <= 2 ? (const void*)gh_ws_write_kernel<WS_U, WS_TB, GL, 2>
+         : ns <= 3 ? (const void*)gh_ws_write_kernel<WS_U, WS_TB, GL, 3>
+         : ns <= 4 ? (const void*)gh_ws_write_kernel<WS_U, WS_TB, GL, 4>
+         : ns <= 6 ? (const void*)gh_ws_write_kernel<WS_U, WS_TB, GL, 6>
+                   : (const void*)gh_ws_write_kernel<WS_U, WS_TB, GL, 8>;
 }
-// NS (store instructions per lane per piece): the typical piece's 16-byte chunks / 64
-static WsKernels ws_kernels(uint32_t K, int ns) {
-  const int g = ms_group(K);
-  return g >= 4 ? ws_pair_ns<4>(ns) : g == 3 ? ws_pair_ns<3>(ns) : ws_pair_ns<2>(ns);
+// Count kernel by its LUT width Kc, write kernel by K and NS (store instructions per
+// lane per piece: the typical piece's 16-byte chunks / 64).
+static WsKernels ws_kernels(uint32_t Kc, uint32_t K, int ns) {
+  const int gc = ms_group(Kc), g = ms_group(K);
+  const void* cnt = gc >= 4 ? (const void*)gh_ws_count_kernel<WS_UC, WS_TBC, 4>
+                    : gc == 3 ? (const void*)gh_ws_count_kernel<WS_UC, WS_TBC, 3>
+                              : (const void*)gh_ws_count_kernel<WS_UC, WS_TBC, 2>;
+  const void* wr = g >= 4 ? ws_write_ns<4>(ns) : g == 3 ? ws_write_ns<3>(ns) : ws_write_ns<2>(ns);
+  return {cnt, wr};
+}
+
+// Count LUT of width Kc (u32 entries b | end mask << 16, see gh_ws_count_kernel): every
+// codeword wholly inside the Kc-bit window, greedily.  Returns the expected bits per
+// lookup on random input bits (for a complete code each codeword then has probability
+// 2^-len, about its frequency in the data it was built for).
+static double ws_count_lut(const Canon& cn, uint32_t Kc, std::vector<uint32_t>* out) {
+  double sum = 0;
+  if (out) out->assign(1u << Kc, 0u);
+  for (uint32_t i = 0; i < (1u << Kc); ++i) {
+    const uint32_t bits = i << (32 - Kc);
+    uint32_t pos = 0, mask = 0;
+    while (pos < Kc) {
+      uint32_t fi = 0;
+      const uint32_t l = canon_decode16(cn, (bits << pos) >> 16, &fi);
+      if (l == 0 || pos + l > Kc) break;
+      pos += l;
+      mask |= 1u << (pos - 1);
+    }
+    sum += pos;
+    if (out) (*out)[i] = pos | (mask << 16);
+  }
+  return sum / (double)(1u << Kc);
+}
+// Kc in [max(maxlen, 2), 13] maximising bits per VALU op of a lookup group: GL lookups
+// of ~7 ops each plus ~11 ops of window shift and mask upkeep per chain.  GH_WS_KC
+// overrides (tests).
+static uint32_t ws_count_bits(const Canon& cn) {
+  const uint32_t lo = std::max<uint32_t>(cn.maxlen, 2);
+  if (const char* e = getenv("GH_WS_KC")) return (uint32_t)std::clamp(atoi(e), (int)lo, 14);
+  uint32_t best = lo;
+  double best_eff = -1;
+  for (uint32_t kc = lo; kc <= 13; ++kc) {  // 14 (64 KiB) measured no faster
+    const int gl = ms_group(kc);
+    const double eff = gl * ws_count_lut(cn, kc, nullptr) / (7.0 * gl + 11.0);
+    if (eff > best_eff * 1.01) {  // prefer the smaller table unless clearly better
+      best_eff = eff;
+      best = kc;
+    }
+  }
+  return best;
 }
 static int ws_ns_for(double avg_seg_bytes) {
   const double chunks = avg_seg_bytes * 64 * WS_U / 16.0 * 1.15 + 2;
@@ -2492,6 +2541,14 @@ static int ws_setup(gh_ctx* c, double avg_seg_bytes) {
   if (int rc = ms_build_luts(c, K)) return rc;
   const size_t lb = c->lut_bytes;
   constexpr int NW = WS_TB / 64;
+  {
+    const uint32_t kc = ws_count_bits(cn);
+    std::vector<uint32_t> lc;
+    ws_count_lut(cn, kc, &lc);
+    GH_HIP(hipMalloc(&c->d_ws_lut_c, 4ull << kc));
+    GH_HIP(hipMemcpy(c->d_ws_lut_c, lc.data(), 4ull << kc, hipMemcpyHostToDevice));
+    c->ws_kc = kc;
+  }
   const uint32_t maxsyms = std::min<uint32_t>(143 / std::max<uint32_t>(cn.minlen, 1) + 1, 255);
   // per-wave staging: at least one chain's worst case (64 segments x maxsyms), and a
   // typical whole block (both chains) with room to spare when the LDS allows
@@ -2513,18 +2570,18 @@ static int ws_setup(gh_ctx* c, double avg_seg_bytes) {
     stage = std::max<size_t>((size_t)atoll(es), (chain_worst + 15) & ~15ull) & ~15ull;
   c->stage_bytes = (uint32_t)stage;
   c->lds = lb + NW * stage;
-  c->lds_count = std::max<size_t>(lb, 64);
+  c->lds_count = std::max<size_t>(4ull << c->ws_kc, 64);
   c->ws_ns = ws_ns_for(avg_seg_bytes);
   if (const char* en = getenv("GH_WS_NS")) c->ws_ns = std::clamp(atoi(en), 2, 8);
-  const WsKernels k = ws_kernels(K, c->ws_ns);
+  const WsKernels k = ws_kernels(c->ws_kc, K, c->ws_ns);
   int pc_c = 0, pc_w = 0;
-  GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc_c, k.count, WS_TB, c->lds_count));
+  GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc_c, k.count, WS_TBC, c->lds_count));
   GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc_w, k.write, WS_TB, c->lds));
   if (pc_c < 1 || pc_w < 1) return fail(GH_E_HIP, "wsplit kernels do not fit on a CU");
   c->ws_nblocks = (uint32_t)ceil_div(c->nseg, (uint64_t)WS_SB);  // superblocks
   const uint64_t wg_blocks = ceil_div(c->ws_nblocks, (uint64_t)NW);  // workgroups that have a superblock
   c->grid = (uint32_t)std::min<uint64_t>((uint64_t)pc_w * c->num_cu, wg_blocks);
-  c->ws_grid_c = (uint32_t)std::min<uint64_t>((uint64_t)pc_c * c->num_cu, wg_blocks);
+  c->ws_grid_c = (uint32_t)std::min<uint64_t>((uint64_t)pc_c * c->num_cu, ceil_div(c->ws_nblocks, (uint64_t)(WS_TBC / 64)));
   if (const char* eg = getenv("GH_WS_GRID")) {  // tests: few workgroups, many blocks per wave
     c->grid = (uint32_t)std::clamp<long>(atol(eg), 1, (long)c->grid);
     c->ws_grid_c = (uint32_t)std::clamp<long>(atol(eg), 1, (long)c->ws_grid_c);
@@ -3068,13 +3125,15 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     static thread_local void* ac[1];
     static thread_local void* aw[1];
     wc = m;
-    wc.lut = c->d_ms_lut_c;
+    wc.lut = (const uint2*)c->d_ws_lut_c;
+    wc.kbits = c->ws_kc;
+    wc.lut_bytes = (uint32_t)(4u << c->ws_kc);
     ww = m;
     ww.lut = c->d_ms_lut_w;
     ac[0] = &wc;
     aw[0] = &ww;
-    const WsKernels wk = ws_kernels(c->ms_k, c->ws_ns);
-    GH_HIP(hipLaunchKernel(wk.count, dim3(c->ws_grid_c), dim3(WS_TB), ac, c->lds_count, st));
+    const WsKernels wk = ws_kernels(c->ws_kc, c->ms_k, c->ws_ns);
+    GH_HIP(hipLaunchKernel(wk.count, dim3(c->ws_grid_c), dim3(WS_TBC), ac, c->lds_count, st));
     GH_HIP(hipLaunchKernel((const void*)gh_ws_scan_kernel, dim3(1), dim3(WS_SCAN_TB), ac, 0, st));
     GH_HIP(hipLaunchKernel(wk.write, dim3(c->grid), dim3(WS_TB), aw, c->lds, st));
   } else if (c->ms) {

@@ -32,7 +32,11 @@
 #ifndef GH_WS_TB
 #define GH_WS_TB 512
 #endif
-constexpr int WS_TB = GH_WS_TB;  // threads per workgroup of the count and write kernels
+constexpr int WS_TB = GH_WS_TB;  // threads per workgroup of the write kernel
+#ifndef GH_WS_TBC
+#define GH_WS_TBC 256
+#endif
+constexpr int WS_TBC = GH_WS_TBC;  // threads per workgroup of the count kernel
 constexpr int WS_U = 2;     // chains per lane of the write kernel (segments per lane per block)
 #ifndef GH_WS_UC
 #define GH_WS_UC 4
@@ -40,6 +44,9 @@ constexpr int WS_U = 2;     // chains per lane of the write kernel (segments per
 constexpr int WS_UC = GH_WS_UC;  // chains per lane of the count kernel
 constexpr int WS_SB = 256;  // segments per superblock: ranges are cut at superblock edges
 constexpr int WS_SCAN_TB = 1024;
+#ifndef GH_WS_BF
+#define GH_WS_BF 1  // branch-free staging: every lane ORs (zero past its end), one 64-bit shift per lookup
+#endif
 #ifndef GH_WS_ABLATE
 #define GH_WS_ABLATE 0  // diagnostic builds only (results wrong): 1 no LDS OR, 2 no stores, 4 no copy-out
 #endif
@@ -107,12 +114,31 @@ __device__ __forceinline__ void ws_lut_to_lds(const WsParams& p, uint8_t* smem, 
   for (uint32_t i = tid; i < p.lut_bytes / 16; i += TBK) s4[i] = g[i];
 }
 
+// Count-LUT lookup results: ds_read_b32 each, one wait for the U of a step.
+template <int U>
+__device__ __forceinline__ void ws_wait32(uint32_t (&v)[U]) {
+  static_assert(U == 1 || U == 2 || U == 4, "ws_wait32: 1, 2 or 4 lookups");
+  if constexpr (U == 1) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0])::"memory");
+  } else if constexpr (U == 2) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1])::"memory");
+  } else {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3])::"memory");
+  }
+}
+
+// The count kernel's LUT (its own width Kc <= 14, u32 entries, 4 << Kc bytes): entry
+// = b | endmask << 16, b = bits of the complete codewords in the Kc-bit window (all
+// of them, no cap), end-mask bit e-1 per codeword end e.  One lookup step:
+//   cnt += popcount(endmask & rm)   (SDWA AND of the high half, v_bcnt)
+//   rm >>= b                        (v_ashrrev reads only the low 5 bits of the entry)
+//   q -= entry                      (q's low 16 bits stay exact: sum of b <= 32)
 template <int U, int TBK, int GL>
 __global__ __launch_bounds__(TBK) void gh_ws_count_kernel(const WsParams p) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int tid = threadIdx.x, lane = tid & 63;
-  const uint32_t sh = 29u - p.kbits;  // index bits -> byte offset of a u64 entry
-  const uint32_t amask = ((1u << p.kbits) - 1u) << 3;
+  const uint32_t sh = 30u - p.kbits;  // index bits -> byte offset of a u32 entry
+  const uint32_t amask = ((1u << p.kbits) - 1u) << 2;
   ws_lut_to_lds<TBK>(p, smem, tid);
   if (tid == 0 && (uint32_t)(size_t)(const __attribute__((address_space(3))) uint8_t*)smem != 0u)
     atomicOr(p.status, (unsigned)GH_ST_LAYOUT);
@@ -151,25 +177,28 @@ __global__ __launch_bounds__(TBK) void gh_ws_count_kernel(const WsParams p) {
         }
   #pragma unroll
         for (int j = 0; j < GL; ++j) {
-          uint2 e[U];
+          uint32_t e[U];
   #pragma unroll
           for (int u = 0; u < U; ++u) {
             const uint32_t x = j == 0 ? v[u].d0 : __builtin_amdgcn_alignbit(v[u].d0, v[u].d1, q[u]);
-            e[u] = ms_lds_u64((x >> sh) & amask);
+            asm volatile("ds_read_b32 %0, %1" : "=v"(e[u]) : "v"((x >> sh) & amask) : "memory");
           }
-          ms_wait(e);
+          ws_wait32(e);
   #pragma unroll
           for (int u = 0; u < U; ++u) {
-            cnt[u] = __builtin_popcount(e[u].y & rm[u]) + cnt[u];
-            rm[u] = (uint32_t)((int)rm[u] >> e[u].x);
-            q[u] -= e[u].x;
+            uint32_t m;
+            asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD"
+                : "=v"(m) : "v"(e[u]), "v"(rm[u]));
+            cnt[u] = __builtin_popcount(m) + cnt[u];
+            asm("v_ashrrev_i32 %0, %1, %0" : "+v"(rm[u]) : "v"(e[u]));
+            q[u] -= e[u];
           }
         }
         bool more = false;
   #pragma unroll
         for (int u = 0; u < U; ++u) {
-          ms_shift(v[u], q[u]);
-          R[u] -= 32 - (int)q[u];
+          ms_shift(v[u], q[u]);  // consumed = 32 - (q & 0xFFFF), 2..32: v_alignbit reads q & 31
+          R[u] -= 32 - (int)(q[u] & 0xFFFFu);
           more |= R[u] > 0;
         }
         if (!__any(more)) break;
@@ -215,6 +244,15 @@ __global__ __launch_bounds__(WS_SCAN_TB) void gh_ws_scan_kernel(const WsParams p
     run += t;
   }
   if (tid == 0) *p.total = all;
+}
+
+// OR the four bytes v at LDS byte address a (any alignment) into the two aligned
+// dwords it spans: one 64-bit shift, two ds_or_b32, no branch (v = 0 is a no-op).
+__device__ __forceinline__ void ws_lds_or4(uint32_t a, uint32_t v) {
+  const unsigned long long d = (unsigned long long)v << ((a & 3u) << 3);
+  asm volatile("ds_or_b32 %0, %1\n\tds_or_b32 %0, %2 offset:4" ::"v"(a & ~3u), "v"((uint32_t)d),
+               "v"((uint32_t)(d >> 32))
+               : "memory");
 }
 
 // Byte-exact store of staging chunk bytes [k0, k1) of one 16-byte chunk (lanes 0..15).
@@ -316,8 +354,9 @@ __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
         for (int u = 0; u < U; ++u) {
           const bool on = nh == 1 || (uint32_t)u == h;
           v[u] = make_win(wc[u], w4c[u], start[u]);
-          ptr[u] = on ? stage0 + 16u + lb + (nh == 1 ? coff[u] : 0u) + bpos[u] : 0u;
-          end[u] = on ? ptr[u] + cc[u] : 0u;
+          // a chain not staged in this piece: an empty range inside the staging
+          ptr[u] = on ? stage0 + 16u + lb + (nh == 1 ? coff[u] : 0u) + bpos[u] : stage0 + 4u * (uint32_t)lane;
+          end[u] = on ? ptr[u] + cc[u] : ptr[u];
         }
         for (int g = 0; g < 160; ++g) {
           uint32_t q[U];
@@ -334,7 +373,13 @@ __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
             ms_wait(e);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-              if (!(GH_WS_ABLATE & 1) && ptr[u] < end[u]) ms_lds_or_bytes(ptr[u], e[u].x);
+              if constexpr (GH_WS_BF) {
+                // a lane past its end ORs zero at its end (inside the staging spill)
+                const bool on = ptr[u] < end[u];
+                if (!(GH_WS_ABLATE & 1)) ws_lds_or4(on ? ptr[u] : end[u], on ? e[u].x : 0u);
+              } else if (!(GH_WS_ABLATE & 1) && ptr[u] < end[u]) {
+                ms_lds_or_bytes(ptr[u], e[u].x);
+              }
               ptr[u] = ms_add_n(ptr[u], e[u].y);
               q[u] -= e[u].y;
             }
