@@ -88,6 +88,18 @@ __global__ __launch_bounds__(ETB) void gh_enc_hist_kernel(const uint8_t* in, uin
   }
 }
 
+// Inclusive wave scan on the VALU with DPP (row_shr 1/2/4/8 within 16-lane rows,
+// row_bcast 15/31 across them): no LDS round trips, unlike ds_bpermute shuffles.
+__device__ __forceinline__ uint32_t enc_wave_scan(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);
+  return v;
+}
+
 // Workgroup exclusive scan of one u32 per thread; returns the exclusive prefix and
 // sets total.  s_red: NWAVE u32 of LDS.
 __device__ __forceinline__ uint32_t enc_block_scan(uint32_t x, uint32_t* s_red, uint32_t& total) {
@@ -211,41 +223,60 @@ struct EncParams {
   const unsigned long long* blk_off;   // bit offset of each scan block
   uint32_t* words;                     // W payload words
   uint32_t* gaps;                      // GW gap words, zeroed
+  uint32_t* junk;                      // one dword per thread of the grid (padding stores)
   uint64_t n;
   uint32_t nchunks;
 };
 
+constexpr int ELREP = 16;  // write-kernel LUT replicas (lane & 15): a lookup collides at most 2-way
+
+// A thread's 16 codewords, combined in registers: LUT entries hold the code
+// left-aligned, e = code << (32 - len) | len (len <= 16 sits in the low 5 bits, below
+// the code), so a pair is one shift and one AND-OR (v_lshrrev reads only the low 5
+// bits of the entry it shifts by), and two pairs make a left-aligned 64-bit quad.
+// Each quad is ORed into the LDS image as up to three words.
+__device__ __forceinline__ uint32_t enc_pair(uint32_t a, uint32_t c, uint32_t& len) {
+  len = (a & 31u) + (c & 31u);
+  return (a & 0xFFFF0000u) | ((c & 0xFFFF0000u) >> (a & 31u));
+}
+
 // Persistent: workgroup b encodes chunks b, b + G, ...  The next chunk's bytes and
 // offset (and the 32 bytes after it, for its last word) are loaded while the current
-// chunk is encoded; the LDS image is re-zeroed as it is written out.
+// chunk is encoded; the LDS image is re-zeroed as it is written out.  NSW: payload
+// store instructions per thread per chunk, a fixed count (padding stores go to the
+// thread's junk dword; words past NSW * ETB loop), plus one gap-word store: loads and
+// stores share one in-order counter (vmcnt), and with a fixed count of stores younger
+// than the prefetch the next chunk waits for its loads with vmcnt(N) instead of also
+// waiting for this chunk's stores.
+template <int NSW>
 __global__ __launch_bounds__(ETB) void gh_enc_write_kernel(const EncParams p) {
-  __shared__ uint32_t s_lut[257];
+  __shared__ uint32_t s_lutr[257 * ELREP];  // left-aligned entries, replicated
   __shared__ uint32_t s_w[EWORDS];
   __shared__ uint32_t s_g[EGAPW];
   __shared__ uint32_t s_red[2][ETB / 64];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const uint32_t lutv = p.lut[tid & 255];
   uint32_t c = blockIdx.x;
   const uint32_t G = gridDim.x;
   // chunk c's inputs: its 16 bytes per lane, its offset, and (last lane) the next 32 bytes
-  uint4 v = make_uint4(0, 0, 0, 0), x0 = v, x1 = v;
-  unsigned long long off0 = 0;
+  uint4 v = make_uint4(0, 0, 0, 0);
+  uint32_t xbyte = 0;
+  unsigned long long offb = 0;  // chunk offset = block part + local part, added at use
+  uint32_t offl = 0;            // (an add here would wait for the loads at once)
+  // every load unconditional and in bounds (the input buffer is padded by ECHUNK + 64
+  // bytes past n; bytes past n are masked by index), so no branch holds a load
   auto fetch = [&](uint32_t cc) {
     const uint64_t ib = (uint64_t)cc * ECHUNK + (uint64_t)tid * EBPT;
-    if (ib + EBPT <= p.n) v = *(const uint4*)(p.in + ib);
-    else v = make_uint4(0, 0, 0, 0);  // tail handled by byte loads below
-    off0 = p.blk_off[cc / SCAN_BLK] + p.chunk_loc[cc];
-    if (tid == ETB - 1) {
-      const uint64_t xb = (uint64_t)(cc + 1) * ECHUNK;
-      if (xb + 2 * EBPT <= p.n) {
-        x0 = *(const uint4*)(p.in + xb);
-        x1 = *(const uint4*)(p.in + xb + EBPT);
-      }
-    }
+    v = *(const uint4*)(p.in + ib);
+    offb = p.blk_off[cc / SCAN_BLK];
+    offl = p.chunk_loc[cc];
+    xbyte = p.in[(uint64_t)(cc + 1) * ECHUNK + (uint64_t)(lane & 31)];  // the next chunk's byte lane & 31
   };
   if (c < p.nchunks) fetch(c);
-  for (int i = tid; i < 256; i += ETB) s_lut[i] = lutv;
-  if (tid == 0) s_lut[256] = 0;
+  for (int i = tid; i < 257 * ELREP; i += ETB) {
+    const uint32_t v = i / ELREP < 256 ? p.lut[i / ELREP] : 0u;
+    const uint32_t l = v & 0xFFu;
+    s_lutr[i] = l ? ((v >> 8) << (32u - l)) | l : 0u;
+  }
   for (int i = tid; i < EWORDS; i += ETB) s_w[i] = 0;
   for (int i = tid; i < EGAPW; i += ETB) s_g[i] = 0;
   __syncthreads();
@@ -253,29 +284,20 @@ __global__ __launch_bounds__(ETB) void gh_enc_write_kernel(const EncParams p) {
     // this chunk's bytes (absent past n: 0x100, length 0)
     const uint64_t ib = (uint64_t)c * ECHUNK + (uint64_t)tid * EBPT;
     uint32_t b[EBPT];
-    if (ib + EBPT <= p.n) {
 #pragma unroll
-      for (int k = 0; k < EBPT; ++k) b[k] = enc_byte(v, k);
-    } else {
-#pragma unroll
-      for (int k = 0; k < EBPT; ++k) b[k] = ib + k < p.n ? (uint32_t)p.in[ib + k] : 0x100u;
-    }
-    uint32_t xw[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+    for (int k = 0; k < EBPT; ++k) b[k] = ib + k < p.n ? enc_byte(v, k) : 0x100u;
+    const uint32_t nx = xbyte;  // this iteration's copy (fetch() overwrites xbyte)
     const uint64_t xb = (uint64_t)(c + 1) * ECHUNK;
-    const bool xfull = xb + 2 * EBPT <= p.n;
-    const unsigned long long o0 = off0;
+    const unsigned long long o0 = offb + offl;
     if (c + G < p.nchunks) fetch(c + G);  // prefetch
-    uint32_t bits = 0;
+    uint32_t e[EBPT], bits = 0;
 #pragma unroll
-    for (int k = 0; k < EBPT; ++k) bits += s_lut[b[k]] & 0xFFu;
+    for (int k = 0; k < EBPT; ++k) e[k] = s_lutr[b[k] * ELREP + (tid & (ELREP - 1))];
+#pragma unroll
+    for (int k = 0; k < EBPT; ++k) bits += e[k] & 31u;
     // block scan (double-buffered wave sums: the barrier also orders the previous
     // iteration's write-out and re-zeroing before this iteration's OR-s)
-    uint32_t incl = bits;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t y = __shfl_up(incl, d, 64);
-      if (lane >= d) incl += y;
-    }
+    const uint32_t incl = enc_wave_scan(bits);
     if (lane == 63) s_red[it & 1][wid] = incl;
     __syncthreads();
     uint32_t before = 0, cbits = 0;
@@ -291,44 +313,72 @@ __global__ __launch_bounds__(ETB) void gh_enc_write_kernel(const EncParams p) {
     const unsigned long long B = o0 & ~1023ull;
     const uint32_t qs = (uint32_t)(o0 - B);  // chunk start
     const uint32_t qend = qs + cbits;        // chunk end (the next chunk's first bit)
-    uint32_t q = qs + excl;
-    uint32_t lw = q >> 5;                    // LDS word being filled
-    int nb = (int)(q & 31);                  // pending bits in acc (the first q & 31 are zeros)
-    uint64_t acc = 0;
-    auto put = [&](uint32_t e) {
-      const uint32_t l = e & 0xFFu;
-      const uint32_t qe = q + l;
-      if ((qe ^ q) >= 128u) {  // crosses a 128-bit boundary
-        const uint32_t gv = qe & 15u;  // nibble of segment q >> 7
-        if (gv && q < qend) atomicOr(&s_g[q >> 10], gv << (4 * ((q >> 7) & 7u)));
-      }
-      acc = (acc << l) | (e >> 8);
-      nb += (int)l;
-      if (nb >= 32) {
-        nb -= 32;
-        atomicOr(&s_w[lw], (uint32_t)(acc >> nb));
-        ++lw;
-      }
-      q = qe;
-    };
+    const uint32_t q0 = qs + excl;           // this thread's first bit
+    // pairs and quads (left-aligned), the quads ORed into the image
+    uint32_t pl[EBPT / 2], pv[EBPT / 2];
 #pragma unroll
-    for (int k = 0; k < EBPT; ++k) put(s_lut[b[k]]);
-    if (tid == ETB - 1) {
-      // complete the chunk's last word with the next chunk's first symbols (their gap
-      // nibbles belong to that chunk: q >= qend skips them)
+    for (int j = 0; j < EBPT / 2; ++j) pv[j] = enc_pair(e[2 * j], e[2 * j + 1], pl[j]);
+    uint32_t qa = q0, qe[EBPT / 4];
+#pragma unroll
+    for (int i = 0; i < EBPT / 4; ++i) {
+      const uint32_t l0 = pl[2 * i], m = l0 + pl[2 * i + 1];
+      const unsigned long long Q = ((unsigned long long)pv[2 * i] << 32) |
+                                   ((unsigned long long)pv[2 * i + 1] << (32u - l0));
+      const uint32_t hi = (uint32_t)(Q >> 32), lo = (uint32_t)Q, sft = qa & 31u;
+      uint32_t* wp = &s_w[qa >> 5];
+      if (m) atomicOr(wp, hi >> sft);
+      if (sft + m > 32u) atomicOr(wp + 1, __builtin_amdgcn_alignbit(hi, lo, sft));
+      if (sft + m > 64u) atomicOr(wp + 2, __builtin_amdgcn_alignbit(lo, 0u, sft));
+      qa += m;
+      qe[i] = qa;
+    }
+    // gap nibbles: for each 128-bit boundary strictly inside [q0, qa), the codeword
+    // holding bits bd-1 and bd (quad, then pair, then codeword by compare-selects)
+    for (uint32_t bd = ((q0 >> 7) + 1u) << 7; bd < qa; bd += 128u) {
+      const bool i0 = bd >= qe[0], i1 = bd >= qe[1], i2 = bd >= qe[2];
+      const uint32_t qs4 = i2 ? qe[2] : i1 ? qe[1] : i0 ? qe[0] : q0;
+      const uint32_t la = i2 ? pl[6] : i1 ? pl[4] : i0 ? pl[2] : pl[0];
+      const uint32_t lb = i2 ? pl[7] : i1 ? pl[5] : i0 ? pl[3] : pl[1];
+      const uint32_t ea = i2 ? e[12] : i1 ? e[8] : i0 ? e[4] : e[0];
+      const uint32_t eb = i2 ? e[14] : i1 ? e[10] : i0 ? e[6] : e[2];
+      const bool second = bd >= qs4 + la;  // in the quad's second pair
+      const uint32_t ps = second ? qs4 + la : qs4;
+      const uint32_t lp = second ? lb : la;
+      const uint32_t l1 = (second ? eb : ea) & 31u;  // the pair's first codeword
+      const bool c2 = bd >= ps + l1;
+      const uint32_t cs = c2 ? ps + l1 : ps;        // codeword start
+      const uint32_t ce = c2 ? ps + lp : ps + l1;   // codeword end
+      const uint32_t gv = ce & 15u;
+      if (cs < bd && gv && cs < qend) atomicOr(&s_g[cs >> 10], gv << (4 * ((cs >> 7) & 7u)));
+    }
+    if (wid == ETB / 64 - 1) {
+      // complete the chunk's last word (bits [qend, wend)) with the next chunk's first
+      // codewords, one per lane (lanes 0..31: bytes 0..31, codes >= 1 bit); their gap
+      // nibbles belong to the next chunk
       const uint32_t wend = (qend + 31u) & ~31u;
-      for (uint32_t k = 0; q < wend && xb + k < p.n; ++k) {
-        const uint32_t byte = xfull ? (xw[(k >> 2) & 7] >> (8 * (k & 3))) & 0xFFu : (uint32_t)p.in[xb + k];
-        put(s_lut[byte]);
+      const uint32_t ex = (lane < 32 && xb + (uint32_t)lane < p.n) ? s_lutr[nx * ELREP + (tid & (ELREP - 1))] : 0u;
+      const uint32_t lx = ex & 31u;
+      const uint32_t st = qend + enc_wave_scan(lx) - lx;  // this codeword's first bit
+      if (lx && st < wend) {
+        const uint32_t cw = ex & 0xFFFF0000u, sh = st & 31u;  // left-aligned code
+        atomicOr(&s_w[st >> 5], cw >> sh);
+        if (sh + lx > 32u) atomicOr(&s_w[(st >> 5) + 1], cw << (32u - sh));
       }
     }
-    if (nb > 0) atomicOr(&s_w[lw], (uint32_t)(acc << (32 - nb)));
     __syncthreads();
     // payload words whose first bit lies in [o0, o0 + cbits): local [w0, w1); the
     // image is zeroed as it is read (up to the completion word)
     const uint32_t w0 = (qs + 31u) >> 5, w1 = (qend + 31u) >> 5;
     uint32_t* wout = p.words + (B >> 5);
-    for (uint32_t i = tid; i <= w1; i += ETB) {
+    uint32_t* junk = p.junk + (size_t)blockIdx.x * ETB + tid;
+#pragma unroll
+    for (int j = 0; j < NSW; ++j) {
+      const uint32_t i = (uint32_t)tid + (uint32_t)(ETB * j);
+      const uint32_t x = s_w[i < (uint32_t)EWORDS ? i : 0u];
+      if (i <= w1) s_w[i] = 0;
+      *((i >= w0 && i < w1) ? wout + i : junk) = x;
+    }
+    for (uint32_t i = tid + ETB * NSW; i <= w1; i += ETB) {
       const uint32_t x = s_w[i];
       s_w[i] = 0;
       if (i >= w0 && i < w1) wout[i] = x;
@@ -337,15 +387,14 @@ __global__ __launch_bounds__(ETB) void gh_enc_write_kernel(const EncParams p) {
     // hold nibbles of the neighbouring chunks
     const uint32_t g1 = cbits ? (qend - 1u) >> 10 : 0u;
     uint32_t* gout = p.gaps + (B >> 10);
-    for (uint32_t i = tid; i <= g1; i += ETB) {
-      const uint32_t x = s_g[i];
-      s_g[i] = 0;
-      if (!cbits) continue;
-      if (i == 0 || i == g1) {
-        if (x) atomicOr(&gout[i], x);
-      } else {
-        gout[i] = x;
-      }
+    static_assert(EGAPW <= ETB, "one gap word per thread");
+    {
+      const uint32_t i = (uint32_t)tid;
+      const uint32_t x = s_g[i < (uint32_t)EGAPW ? i : 0u];
+      if (i <= g1) s_g[i] = 0;
+      const bool in = cbits && i <= g1, edge = i == 0 || i == g1;
+      *((in && !edge) ? gout + i : junk) = x;  // interior: a plain store (always issued)
+      if (in && edge && x) atomicOr(&gout[i], x);
     }
   }
 }
@@ -374,6 +423,8 @@ struct gh_ectx {
   uint64_t chunk_cap = 0;
   uint32_t* d_words = nullptr;
   uint32_t* d_gaps = nullptr;
+  uint32_t* d_junk = nullptr;              // write kernel padding stores: one dword per thread
+  uint64_t junk_cap = 0;
   uint64_t words_cap = 0, gaps_cap = 0;
   gh_encode_plan plan{};
   bool planned = false, encoded = false;
@@ -409,7 +460,7 @@ extern "C" int gh_ectx_destroy(gh_ectx* e) {
   (void)hipSetDevice(e->device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   for (void* p : {(void*)e->d_in, (void*)e->d_count, (void*)e->d_lut, (void*)e->d_chunk_bits,
-                  (void*)e->d_chunk_off, (void*)e->d_words, (void*)e->d_gaps})
+                  (void*)e->d_chunk_off, (void*)e->d_words, (void*)e->d_gaps, (void*)e->d_junk})
     (void)hipFree(p);
   if (e->ev0) (void)hipEventDestroy(e->ev0);
   if (e->ev1) (void)hipEventDestroy(e->ev1);
@@ -421,12 +472,14 @@ extern "C" int gh_ectx_destroy(gh_ectx* e) {
 extern "C" int gh_ectx_load(gh_ectx* e, const uint8_t* in, uint64_t n) {
   if (!e || (n && !in)) return fail(GH_E_ARG, "null argument");
   GH_EHIP(hipSetDevice(e->device));
-  if (n + 16 > e->in_cap) {
+  // padded: the write kernel's loads are unconditional (up to a chunk + 32 bytes past n)
+  const uint64_t need = n + ECHUNK + 64;
+  if (need > e->in_cap) {
     (void)hipFree(e->d_in);
     e->d_in = nullptr;
     e->in_cap = 0;
-    GH_EHIP(hipMalloc(&e->d_in, n + 16));
-    e->in_cap = n + 16;
+    GH_EHIP(hipMalloc(&e->d_in, need));
+    e->in_cap = need;
   }
   if (n) GH_EHIP(hipMemcpyAsync(e->d_in, in, n, hipMemcpyHostToDevice, e->stream));
   GH_EHIP(hipStreamSynchronize(e->stream));
@@ -498,9 +551,18 @@ extern "C" int gh_ectx_encode(gh_ectx* e, float* kernel_ms) {
   GH_EHIP(hipEventRecord(e->ev0, e->stream));
   GH_EHIP(hipMemsetAsync(e->d_gaps, 0, 4 * (GW + 4), e->stream));
   if (nchunks) {
+    // payload words per chunk ~ 4096 * W / n: NSW = store instructions per thread
+    const double wpc = (double)ECHUNK * (double)pl.w / (double)std::max<uint64_t>(e->n, 1) + 2.0;
+    const int need = (int)std::ceil(wpc * 1.05 / ETB);
+    const void* wk = need <= 1   ? (const void*)gh_enc_write_kernel<1>
+                     : need <= 2 ? (const void*)gh_enc_write_kernel<2>
+                     : need <= 3 ? (const void*)gh_enc_write_kernel<3>
+                     : need <= 4 ? (const void*)gh_enc_write_kernel<4>
+                     : need <= 6 ? (const void*)gh_enc_write_kernel<6>
+                                 : (const void*)gh_enc_write_kernel<9>;
     int pb = 0, pw = 0;  // persistent grids: what is resident at once
     GH_EHIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pb, (const void*)gh_enc_bits_kernel, ETB, 0));
-    GH_EHIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pw, (const void*)gh_enc_write_kernel, ETB, 0));
+    GH_EHIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pw, wk, ETB, 0));
     const uint32_t gb = (uint32_t)std::min<uint64_t>(nchunks, (uint64_t)std::max(pb, 1) * e->num_cu);
     hipLaunchKernelGGL(gh_enc_bits_kernel, dim3(gb), dim3(ETB), 0, e->stream, e->d_in, e->n, (uint32_t)nchunks,
                        e->d_lut, e->d_chunk_bits);
@@ -510,9 +572,17 @@ extern "C" int gh_ectx_encode(gh_ectx* e, float* kernel_ms) {
     hipLaunchKernelGGL(gh_enc_scan_kernel, dim3(nblk), dim3(SCAN_TB), 0, e->stream, e->d_chunk_bits,
                        (uint32_t)nchunks, loc, blk);
     hipLaunchKernelGGL(gh_enc_blkscan_kernel, dim3(1), dim3(SCAN_TB), 0, e->stream, blk, nblk);
-    EncParams p{e->d_in, e->d_lut, loc, blk, e->d_words, e->d_gaps, e->n, (uint32_t)nchunks};
     const uint32_t gw = (uint32_t)std::min<uint64_t>(nchunks, (uint64_t)std::max(pw, 1) * e->num_cu);
-    hipLaunchKernelGGL(gh_enc_write_kernel, dim3(gw), dim3(ETB), 0, e->stream, p);
+    if ((uint64_t)gw * ETB > e->junk_cap) {
+      (void)hipFree(e->d_junk);
+      e->d_junk = nullptr;
+      e->junk_cap = 0;
+      GH_EHIP(hipMalloc(&e->d_junk, 4ull * gw * ETB));
+      e->junk_cap = (uint64_t)gw * ETB;
+    }
+    EncParams p{e->d_in, e->d_lut, loc, blk, e->d_words, e->d_gaps, e->d_junk, e->n, (uint32_t)nchunks};
+    void* args[] = {&p};
+    GH_EHIP(hipLaunchKernel(wk, dim3(gw), dim3(ETB), args, 0, e->stream));
     GH_EHIP(hipGetLastError());
   }
   GH_EHIP(hipEventRecord(e->ev1, e->stream));
