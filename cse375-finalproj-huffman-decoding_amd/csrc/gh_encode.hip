@@ -123,34 +123,52 @@ __device__ __forceinline__ uint32_t enc_block_scan(uint32_t x, uint32_t* s_red, 
   return before + incl - x;
 }
 
-// Persistent: workgroup b takes chunks b, b + G, ...; the next chunk's bytes are
-// loaded before the current one's reduction.
+// Persistent: workgroup b takes chunk pairs (b + 2kG, b + (2k+1)G); the next pair's
+// bytes (two 16-byte loads per thread: the bytes in flight per CU set this kernel's
+// bandwidth) are loaded before the current pair's reduction.  Loads are unconditional
+// (chunk index clamped, input padded past n), bytes past n masked by index.
 __global__ __launch_bounds__(ETB) void gh_enc_bits_kernel(const uint8_t* in, uint64_t n, uint32_t nchunks,
                                                           const uint32_t* lut, uint32_t* chunk_bits) {
-  __shared__ uint32_t s_len[257];
-  __shared__ uint32_t s_red[2][ETB / 64];
+  __shared__ uint32_t s_len[256];
+  __shared__ uint32_t s_red[2][2][ETB / 64];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   for (int i = tid; i < 256; i += ETB) s_len[i] = lut[i] & 0xFFu;
-  if (tid == 0) s_len[256] = 0;
-  uint32_t b[EBPT];
-  uint32_t c = blockIdx.x;
-  if (c < nchunks) enc_load(in, n, (uint64_t)c * ECHUNK + (uint64_t)tid * EBPT, b);
-  __syncthreads();
-  for (uint32_t it = 0; c < nchunks; c += gridDim.x, ++it) {
+  const uint32_t G = gridDim.x;
+  auto ld = [&](uint32_t cc) {
+    return *(const uint4*)(in + (uint64_t)min(cc, nchunks - 1) * ECHUNK + (uint64_t)tid * EBPT);
+  };
+  auto chunk_bits_of = [&](const uint4& v, uint32_t cc) {
+    const uint64_t ib = (uint64_t)cc * ECHUNK + (uint64_t)tid * EBPT;
     uint32_t bits = 0;
+    if (ib + EBPT <= n) {
 #pragma unroll
-    for (int k = 0; k < EBPT; ++k) bits += s_len[b[k]];
-    const uint32_t cn = c + gridDim.x;
-    if (cn < nchunks) enc_load(in, n, (uint64_t)cn * ECHUNK + (uint64_t)tid * EBPT, b);
+      for (int k = 0; k < EBPT; ++k) bits += s_len[enc_byte(v, k)];
+    } else {
+      const uint32_t rem = ib < n ? (uint32_t)(n - ib) : 0u;
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) bits += __shfl_xor(bits, d, 64);
-    if (lane == 0) s_red[it & 1][wid] = bits;
-    __syncthreads();  // (double-buffered partial sums: one barrier per chunk)
-    if (tid == 0) {
+      for (int k = 0; k < EBPT; ++k) bits += (uint32_t)k < rem ? s_len[enc_byte(v, k)] : 0u;
+    }
+    return bits;
+  };
+  uint32_t c = blockIdx.x;
+  uint4 va = ld(c), vb = ld(c + G);
+  __syncthreads();
+  for (uint32_t it = 0; c < nchunks; c += 2 * G, ++it) {
+    const uint32_t ba = chunk_bits_of(va, c), bb = chunk_bits_of(vb, c + G);
+    va = ld(c + 2 * G);
+    vb = ld(c + 3 * G);
+    const uint32_t sa = enc_wave_scan(ba), sb = enc_wave_scan(bb);  // lane 63: wave totals
+    if (lane == 63) {
+      s_red[it & 1][0][wid] = sa;
+      s_red[it & 1][1][wid] = sb;
+    }
+    __syncthreads();  // (double-buffered partial sums: one barrier per pair)
+    if (tid < 2) {
       uint32_t t = 0;
 #pragma unroll
-      for (int q = 0; q < ETB / 64; ++q) t += s_red[it & 1][q];
-      chunk_bits[c] = t;
+      for (int q = 0; q < ETB / 64; ++q) t += s_red[it & 1][tid][q];
+      const uint32_t cc = c + (uint32_t)tid * G;
+      if (cc < nchunks) chunk_bits[cc] = t;
     }
   }
 }
@@ -284,8 +302,14 @@ __global__ __launch_bounds__(ETB) void gh_enc_write_kernel(const EncParams p) {
     // this chunk's bytes (absent past n: 0x100, length 0)
     const uint64_t ib = (uint64_t)c * ECHUNK + (uint64_t)tid * EBPT;
     uint32_t b[EBPT];
+    if (ib + EBPT <= p.n) {  // (divergent only in the last chunk)
 #pragma unroll
-    for (int k = 0; k < EBPT; ++k) b[k] = ib + k < p.n ? enc_byte(v, k) : 0x100u;
+      for (int k = 0; k < EBPT; ++k) b[k] = enc_byte(v, k);
+    } else {
+      const uint32_t rem = ib < p.n ? (uint32_t)(p.n - ib) : 0u;
+#pragma unroll
+      for (int k = 0; k < EBPT; ++k) b[k] = (uint32_t)k < rem ? enc_byte(v, k) : 0x100u;
+    }
     const uint32_t nx = xbyte;  // this iteration's copy (fetch() overwrites xbyte)
     const uint64_t xb = (uint64_t)(c + 1) * ECHUNK;
     const unsigned long long o0 = offb + offl;
