@@ -318,3 +318,25 @@ def test_wave_split_repeated_and_default(gpu, orc, grid, monkeypatch):
                 assert gpu.PATH_NAMES[rep.path] == "multi_wave" and rep.status == 0
                 assert rep.symbols >= n
                 assert np.array_equal(d.download(n), data)
+
+
+@pytest.mark.parametrize("kc", ["2", "11", "12", "13", "14"])
+def test_wave_split_count_lut_widths(gpu, orc, kc, monkeypatch):
+    """The wave split's count LUT at every width it can take (GH_WS_KC, clamped up to
+    maxlen): u32 entries b | end mask << 16 hold every complete codeword of the window,
+    up to 7 on 2-bit codes at 14 bits.  Per-segment totals must equal the reference
+    segment rule's (decoder.cu:529-569) and the bytes the oracle's decode."""
+    monkeypatch.setenv("GH_MODE", "wsplit")
+    monkeypatch.setenv("GH_WS_KC", kc)
+    for seed, r, n in ((61, 0.9, 300_007), (62, 0.5, 200_003), (63, 0.99, 77_777), (64, 0.1, 50_001)):
+        data = gpu.generate(seed, r, n)
+        img = _roundtrip(gpu, orc, data)
+        s = gpu.parse(img)
+        with gpu.Decoder(0) as d:
+            d.load(s)
+            d.decode()
+            rep = d.report()
+        if max(l for _, l in s.symbols) <= 12:
+            assert gpu.PATH_NAMES[rep.path] == "multi_wave"
+        if n < 100_000:
+            assert rep.symbols == sum(orc.segment_count(img, i) for i in range(s.g))
