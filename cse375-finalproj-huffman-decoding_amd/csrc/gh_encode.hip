@@ -267,7 +267,7 @@ __device__ __forceinline__ uint32_t enc_pair(uint32_t a, uint32_t c, uint32_t& l
 // than the prefetch the next chunk waits for its loads with vmcnt(N) instead of also
 // waiting for this chunk's stores.
 template <int NSW>
-__global__ __launch_bounds__(ETB) void gh_enc_write_kernel(const EncParams p) {
+__global__ __launch_bounds__(ETB) __attribute__((amdgpu_waves_per_eu(6))) void gh_enc_write_kernel(const EncParams p) {
   __shared__ uint32_t s_lutr[257 * ELREP];  // left-aligned entries, replicated
   __shared__ uint32_t s_w[EWORDS];
   __shared__ uint32_t s_g[EGAPW];
