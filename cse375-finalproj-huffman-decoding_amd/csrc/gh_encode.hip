@@ -123,14 +123,18 @@ __device__ __forceinline__ uint32_t enc_block_scan(uint32_t x, uint32_t* s_red, 
   return before + incl - x;
 }
 
-// Persistent: workgroup b takes chunk pairs (b + 2kG, b + (2k+1)G); the next pair's
-// bytes (two 16-byte loads per thread: the bytes in flight per CU set this kernel's
-// bandwidth) are loaded before the current pair's reduction.  Loads are unconditional
-// (chunk index clamped, input padded past n), bytes past n masked by index.
+// Persistent: workgroup b takes chunk groups (b + EBQ*k*G + j*G, j < EBQ); the next
+// group's bytes (EBQ 16-byte loads per thread: the bytes in flight per CU set this
+// kernel's bandwidth) are loaded before the current group's reduction.  Loads are
+// unconditional (chunk index clamped, input padded past n), bytes past n masked by index.
+#ifndef GH_ENC_BQ
+#define GH_ENC_BQ 2  // chunks in flight per thread (4 measured slower: 246 vs 229 us on cfg4)
+#endif
+constexpr int EBQ = GH_ENC_BQ;
 __global__ __launch_bounds__(ETB) void gh_enc_bits_kernel(const uint8_t* in, uint64_t n, uint32_t nchunks,
                                                           const uint32_t* lut, uint32_t* chunk_bits) {
   __shared__ uint32_t s_len[256];
-  __shared__ uint32_t s_red[2][2][ETB / 64];
+  __shared__ uint32_t s_red[2][EBQ][ETB / 64];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   for (int i = tid; i < 256; i += ETB) s_len[i] = lut[i] & 0xFFu;
   const uint32_t G = gridDim.x;
@@ -151,19 +155,23 @@ __global__ __launch_bounds__(ETB) void gh_enc_bits_kernel(const uint8_t* in, uin
     return bits;
   };
   uint32_t c = blockIdx.x;
-  uint4 va = ld(c), vb = ld(c + G);
+  uint4 v[EBQ];
+#pragma unroll
+  for (int j = 0; j < EBQ; ++j) v[j] = ld(c + (uint32_t)j * G);
   __syncthreads();
-  for (uint32_t it = 0; c < nchunks; c += 2 * G, ++it) {
-    const uint32_t ba = chunk_bits_of(va, c), bb = chunk_bits_of(vb, c + G);
-    va = ld(c + 2 * G);
-    vb = ld(c + 3 * G);
-    const uint32_t sa = enc_wave_scan(ba), sb = enc_wave_scan(bb);  // lane 63: wave totals
-    if (lane == 63) {
-      s_red[it & 1][0][wid] = sa;
-      s_red[it & 1][1][wid] = sb;
+  for (uint32_t it = 0; c < nchunks; c += EBQ * G, ++it) {
+    uint32_t b[EBQ];
+#pragma unroll
+    for (int j = 0; j < EBQ; ++j) b[j] = chunk_bits_of(v[j], c + (uint32_t)j * G);
+#pragma unroll
+    for (int j = 0; j < EBQ; ++j) v[j] = ld(c + (uint32_t)(EBQ + j) * G);
+#pragma unroll
+    for (int j = 0; j < EBQ; ++j) {
+      const uint32_t sc = enc_wave_scan(b[j]);  // lane 63: the wave total
+      if (lane == 63) s_red[it & 1][j][wid] = sc;
     }
-    __syncthreads();  // (double-buffered partial sums: one barrier per pair)
-    if (tid < 2) {
+    __syncthreads();  // (double-buffered partial sums: one barrier per group)
+    if (tid < EBQ) {
       uint32_t t = 0;
 #pragma unroll
       for (int q = 0; q < ETB / 64; ++q) t += s_red[it & 1][tid][q];
