@@ -2535,9 +2535,43 @@ static int ws_ns_for(double avg_seg_bytes) {
   const int ns = (int)std::ceil(chunks / 64);
   return ns <= 2 ? 2 : ns <= 3 ? 3 : ns <= 4 ? 4 : ns <= 6 ? 6 : 8;
 }
+// Write-LUT width of the wave split: K in [max(maxlen, 10), 12] maximising the expected
+// bits per lookup (entries hold up to four codewords, so a wider window helps only codes
+// whose short codewords it can fit more of: r=0.5 codes 7.6 -> 10.4 bits at K 10 -> 12)
+// times lookups per window shift over ~13 ops per lookup plus ~12 per shift; a wider
+// table must win by 5 % (its LDS costs occupancy).  GH_MS_K overrides.
+static uint32_t ws_write_bits(const Canon& cn) {
+  if (getenv("GH_MS_K")) return ms_lut_bits(cn);
+  const uint32_t lo = std::max<uint32_t>(cn.maxlen, 10);
+  uint32_t best = lo;
+  double best_eff = -1;
+  for (uint32_t K = lo; K <= 12; ++K) {
+    double sum = 0;
+    for (uint32_t i = 0; i < (1u << K); ++i) {
+      const uint32_t bits = i << (32 - K);
+      uint32_t pos = 0, n = 0;
+      while (n < 4 && pos < K) {
+        uint32_t fi = 0;
+        const uint32_t l = canon_decode16(cn, (bits << pos) >> 16, &fi);
+        if (l == 0 || pos + l > K) break;
+        pos += l;
+        ++n;
+      }
+      sum += pos;
+    }
+    const int gl = ms_group(K);
+    const double eff = gl * (sum / (double)(1u << K)) / (13.0 * gl + 12.0);
+    if (best_eff < 0 || eff > best_eff * 1.05) {
+      best_eff = eff;
+      best = K;
+    }
+  }
+  return best;
+}
+
 static int ws_setup(gh_ctx* c, double avg_seg_bytes) {
   const Canon& cn = c->canon;
-  const uint32_t K = ms_lut_bits(cn);
+  const uint32_t K = ws_write_bits(cn);
   if (int rc = ms_build_luts(c, K)) return rc;
   const size_t lb = c->lut_bytes;
   constexpr int NW = WS_TB / 64;
