@@ -280,11 +280,11 @@ def test_lean_split_shard_counts(gpu, orc, mode, monkeypatch):
             off += r.symbols
 
 
-@pytest.mark.parametrize("mode", ["tile"])
+@pytest.mark.parametrize("mode", ["tile", "wtile"])
 def test_grouped_split_and_tile(gpu, orc, mode, monkeypatch):
-    """The grouped single-symbol codes (complete, minlen >= 4) through the tile kernel:
-    bytes and symbol totals equal the oracle's (reference segment rule,
-    decoder.cu:529-569)."""
+    """The grouped single-symbol codes (complete, minlen >= 4) through the tile kernel
+    and the wave-tile kernel: bytes and symbol totals equal the oracle's (reference
+    segment rule, decoder.cu:529-569)."""
     monkeypatch.setenv("GH_MODE", mode)
     for seed, n in ((41, 1_000_003), (42, 131_072), (43, 9_999)):
         data = gpu.generate(seed, 0.1, n)
@@ -340,3 +340,48 @@ def test_wave_split_count_lut_widths(gpu, orc, kc, monkeypatch):
             assert gpu.PATH_NAMES[rep.path] == "multi_wave"
         if n < 100_000:
             assert rep.symbols == sum(orc.segment_count(img, i) for i in range(s.g))
+
+
+@pytest.mark.parametrize("percu", ["", "1"])
+def test_wave_tile_repeated_shards_and_cap(gpu, orc, percu, monkeypatch):
+    """The wave-tile kernel (GH_MODE=wtile): back-to-back decodes (timed and not) give
+    identical bytes and totals on the default grid and on one workgroup per CU (more
+    rounds, every workgroup leads several); shards of one stream equal the reference
+    segment rule's counts (decoder.cu:529-569); an output capacity below the shard's
+    total writes exactly the prefix that fits and nothing past it."""
+    monkeypatch.setenv("GH_MODE", "wtile")
+    if percu:
+        monkeypatch.setenv("GH_TILE_PERCU", percu)
+    for seed, n in ((71, 3_000_001), (72, 40_000_003 if not percu else 8_000_017)):
+        data = gpu.generate(seed, 0.1, n)
+        s = gpu.parse(gpu.encode(data))
+        with gpu.Decoder(0) as d:
+            d.load(s)
+            for i in range(4):
+                d.decode(timed=bool(i & 1))
+                rep = d.report()
+                assert gpu.MODE_NAMES[rep.mode] == "wtile" and rep.status == 0
+                assert rep.symbols >= n
+                assert np.array_equal(d.download(n), data)
+    data = gpu.generate(73, 0.1, 700_001)
+    img = gpu.encode(data)
+    s = gpu.parse(img)
+    bounds = gpu.plan_shards(s.g, 3)
+    off = 0
+    for k in range(3):
+        with gpu.Decoder(0) as d:
+            d.load(s, bounds[k], bounds[k + 1])
+            d.decode()
+            r = d.report()
+            assert gpu.MODE_NAMES[r.mode] == "wtile" and r.status == 0
+            assert r.symbols == sum(orc.segment_count(img, i) for i in range(bounds[k], bounds[k + 1]))
+            keep = min(r.symbols, s.n - off)
+            assert np.array_equal(d.download(keep), data[off:off + keep])
+            off += r.symbols
+    for cap in (1, 15, 4097, 333_333):
+        with gpu.Decoder(0) as d:
+            d.load(s, 0, s.g, out_cap=cap)
+            d.decode()
+            r = d.report()
+            assert r.status == 0 and r.out_bytes == cap
+            assert np.array_equal(d.download(cap), data[:cap])
