@@ -1261,6 +1261,9 @@ constexpr int STAGE_PAD = 16;  // staging byte STAGE_PAD + i = tile byte i
 #ifndef GH_TILE_TOPCOPY
 #define GH_TILE_TOPCOPY 0      // with LAG3: copy tile k-3 out at the top of iteration k, before the decode
 #endif
+#ifndef GH_TILE_PRIO
+#define GH_TILE_PRIO 1         // alternate s_setprio between the two workgroup slots of a CU (cfg4 0.747 -> 0.729 ms)
+#endif
 #ifndef GH_LB_MIDG
 #define GH_LB_MIDG 2           // decode group after which the round leader loads aggregates
 #endif
@@ -1590,7 +1593,9 @@ __device__ __forceinline__ void copy_out_tile(uint8_t* out, uint32_t stg, unsign
 // in-order counter (vmcnt); with a fixed store count after the next tile's prefetch
 // loads, the compiler waits for those loads with vmcnt(NS + 1) instead of vmcnt(0),
 // so a wave no longer waits for its previous copy-out's stores to be acknowledged.
-template <int TBK, int NS>
+// LOOP = false: the caller guarantees n + 32 <= 16 * NS * TBK (no chunk beyond the fixed
+// stores), so the store count is the same on every call.
+template <int TBK, int NS, bool LOOP = true>
 __device__ __forceinline__ void copy_out_tile_fixed(uint8_t* out, uint32_t stg, unsigned long long goff, uint32_t n,
                                                     int tid, uint4* junk) {
   const uint32_t lb = (uint32_t)(goff & 15);
@@ -1607,8 +1612,9 @@ __device__ __forceinline__ void copy_out_tile_fixed(uint8_t* out, uint32_t stg, 
     const uint4 v = lds_u128(src + 16u * ((real || have) ? cs : cf));
     *((real || have) ? (uint4*)(o + 16ull * cs) : junk) = v;
   }
-  for (uint32_t c = cf + (uint32_t)tid + (uint32_t)(TBK * NS); c < ce; c += TBK)
-    *(uint4*)(o + 16ull * c) = lds_u128(src + 16u * c);
+  if constexpr (LOOP)
+    for (uint32_t c = cf + (uint32_t)tid + (uint32_t)(TBK * NS); c < ce; c += TBK)
+      *(uint4*)(o + 16ull * c) = lds_u128(src + 16u * c);
   // edge bytes: the head chunk's [lb, min(16, lb + n)) when lb != 0, then the tail
   // chunk's [0, (lb + n) & 15) when it is another chunk; one byte per thread
   const uint32_t nh = (lb && n) ? min(16u, lb + n) - lb : 0u;
@@ -1761,6 +1767,12 @@ void gh_tile_kernel(const TileParams p) {
       break;
     }
     const uint32_t par = k & 1u;
+#if GH_TILE_PRIO
+    // the second workgroup dispatched to a CU loses every issue-arbitration tie to the
+    // first (age order): alternate the two slots' priority by iteration
+    if (((k + (b >= (G >> 1) ? 1u : 0u)) & 1u) != 0u) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+#endif
     STAMP(9);
     // prefix of tile k-2: R[round] + plocal[tile], read by lane 0 of every wave
     // (loaded mid-decode: a load issued at the top often saw the value a little
@@ -2640,17 +2652,28 @@ static int ws_setup(gh_ctx* c, double avg_seg_bytes) {
   return GH_OK;
 }
 
+template <int GRP, int NS, int LPW>
+static const void* wt_kernel_gc(uint32_t kc) {
+  const int gc = ms_group(kc);
+  return gc >= 4 ? (const void*)gh_wtile_kernel<WT_NW, GRP, 4, NS, LPW>
+       : gc == 3 ? (const void*)gh_wtile_kernel<WT_NW, GRP, 3, NS, LPW>
+                 : (const void*)gh_wtile_kernel<WT_NW, GRP, 2, NS, LPW>;
+}
+template <int NS, int LPW>
+static const void* wt_kernel_lpw(uint32_t g, uint32_t kc) {
+  return g >= 4 ? wt_kernel_gc<4, NS, LPW>(kc) : g == 3 ? wt_kernel_gc<3, NS, LPW>(kc) : wt_kernel_gc<2, NS, LPW>(kc);
+}
+// g: decode codewords per window shift; kc: count-LUT width; ns: copy-out stores per lane
+// (4, or 5 for 4-bit codes: 64 U maxsyms + 32 <= 16 * 64 * ns); lpw: window loads per lane
+static const void* wt_kernel_for(uint32_t g, uint32_t kc, int ns, int lpw) {
+  if (ns >= 5) return lpw >= 2 ? wt_kernel_lpw<5, 2>(g, kc) : wt_kernel_lpw<5, 1>(g, kc);
+  return lpw >= 2 ? wt_kernel_lpw<4, 2>(g, kc) : wt_kernel_lpw<4, 1>(g, kc);
+}
+static int wt_ns(uint32_t maxsyms) { return 64u * WT_U * maxsyms + 32 <= 16u * 64 * 4 ? 4 : 5; }
+static int wt_lpw(uint32_t grid) { return grid - 1 > (uint32_t)WT_TB ? 2 : 1; }
+
 // Wave-tile kernel (gh_wtile.hip) for grouped single-symbol codes: complete, every
 // codeword within K <= 12 bits and >= 4 bits (<= 32 symbols per segment).
-static const void* wt_kernel_for(uint32_t g, int lpw) {
-  if (lpw >= 2)
-    return g >= 4 ? (const void*)gh_wtile_kernel<WT_NW, 4, GH_WT_NS, 2>
-         : g == 3 ? (const void*)gh_wtile_kernel<WT_NW, 3, GH_WT_NS, 2>
-                  : (const void*)gh_wtile_kernel<WT_NW, 2, GH_WT_NS, 2>;
-  return g >= 4 ? (const void*)gh_wtile_kernel<WT_NW, 4, GH_WT_NS, 1>
-       : g == 3 ? (const void*)gh_wtile_kernel<WT_NW, 3, GH_WT_NS, 1>
-                : (const void*)gh_wtile_kernel<WT_NW, 2, GH_WT_NS, 1>;
-}
 static int wt_setup(gh_ctx* c) {
   const uint32_t K = c->tables.K;
   c->tile_g = std::min<uint32_t>(4, 32 / std::max<uint32_t>(c->canon.maxlen, 1));
@@ -2658,18 +2681,29 @@ static int wt_setup(gh_ctx* c) {
   for (uint32_t i = 0; i < (1u << K); ++i) lt[i] = c->tables.lut2[i].x | c->tables.lut2[i].y;
   GH_HIP(hipMalloc(&c->d_lut_t, 4ull << K));
   GH_HIP(hipMemcpy(c->d_lut_t, lt.data(), 4ull << K, hipMemcpyHostToDevice));
+  // count LUT (the wave split's end-mask entries), at most 12 bits (16 KiB of LDS)
+  {
+    const uint32_t kc = std::min<uint32_t>(ws_count_bits(c->canon), std::max<uint32_t>(12, c->canon.maxlen));
+    std::vector<uint32_t> lc;
+    ws_count_lut(c->canon, kc, &lc);
+    GH_HIP(hipMalloc(&c->d_ws_lut_c, 4ull << kc));
+    GH_HIP(hipMemcpy(c->d_ws_lut_c, lc.data(), 4ull << kc, hipMemcpyHostToDevice));
+    c->ws_kc = kc;
+  }
+  const size_t lutc_bytes = 4ull << c->ws_kc;
   // one staging buffer holds a wave tile's worst case (64 U segments x maxsyms)
   c->stage_bytes =
       (uint32_t)((STAGE_PAD + 64ull * WT_U * c->tables.maxsyms_seg + 32 + 15) & ~15ull);
-  // LUT replication 2^lgr: the largest that keeps the best occupancy
-  const void* kern = wt_kernel_for(c->tile_g, 2);
+  // decode-LUT replication 2^lgr: the largest that keeps the best occupancy
+  if (64ull * WT_U * c->tables.maxsyms_seg + 32 > 16ull * 64 * 5) return fail(GH_E_HIP, "wave tile too large");
+  const void* kern = wt_kernel_for(c->tile_g, c->ws_kc, wt_ns(c->tables.maxsyms_seg), 2);
   const char* envr = getenv("GH_LGR");
   const int lg = envr ? std::clamp(atoi(envr), 0, 14 - (int)K) : std::min(4, 14 - (int)K);
   int best = 0, best_lg = 0;
   for (int l2 = lg; l2 >= 0; --l2) {
     int pc = 0;
-    GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, kern, WT_TB,
-                                                        wt_lds_bytes<WT_NW>(4ull << (K + l2), c->stage_bytes)));
+    GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &pc, kern, WT_TB, wt_lds_bytes<WT_NW>(4ull << (K + l2), lutc_bytes, c->stage_bytes)));
     if (pc > best) {
       best = pc;
       best_lg = l2;
@@ -2679,12 +2713,12 @@ static int wt_setup(gh_ctx* c) {
   if (best < 1) return fail(GH_E_HIP, "wave-tile kernel does not fit on a CU");
   c->lgr = (uint32_t)best_lg;
   c->lut_bytes = 4ull << (K + best_lg);
-  c->lds = wt_lds_bytes<WT_NW>(c->lut_bytes, c->stage_bytes);
+  c->lds = wt_lds_bytes<WT_NW>(c->lut_bytes, lutc_bytes, c->stage_bytes);
   c->ntiles = (uint32_t)ceil_div(c->nseg, (uint64_t)64 * WT_U * WT_NW);
   c->wt_ntw = (uint32_t)ceil_div(c->nseg, (uint64_t)64 * WT_U);
   int per_cu = best;
   if (const char* ep = getenv("GH_TILE_PERCU")) per_cu = std::clamp(atoi(ep), 1, per_cu);  // diagnostics
-  // each lane of the grid's windows loads at most two aggregates: G - 1 <= 2 * 64 * NW
+  // each lane of a workgroup loads at most two aggregates of a window: G - 1 <= 2 * 64 * NW
   c->grid = (uint32_t)std::min<uint64_t>({(uint64_t)c->ntiles, (uint64_t)per_cu * c->num_cu,
                                           (uint64_t)2 * WT_TB + 1});
   c->tb = WT_TB;
@@ -2762,8 +2796,11 @@ extern "C" int gh_ctx_create(int device, gh_ctx** out) {
       (void)hipFuncSetAttribute(tile_kernel_for(tp, gv), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024);
   for (uint32_t gv : {2u, 3u, 4u})
-    for (int lpw : {1, 2})
-      (void)hipFuncSetAttribute(wt_kernel_for(gv, lpw), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    for (uint32_t kc : {7u, 10u, 12u})
+      for (int ns : {4, 5})
+        for (int lpw : {1, 2})
+          (void)hipFuncSetAttribute(wt_kernel_for(gv, kc, ns, lpw), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    160 * 1024);
   for (int gv : {0, 2, 3, 4})
     for (bool sg : {false, true})
       for (bool fbv : {false, true})
@@ -3061,7 +3098,7 @@ extern "C" int gh_ctx_load(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e
                      hipMemcpyHostToDevice));
   c->gap_nib0 = (uint32_t)(b - 8 * gw0);
   c->ms_last_end = 0;
-  if ((c->ms || c->ws) && e == s->g) {
+  if ((c->ms || c->ws || c->wt) && e == s->g) {
     uint32_t w5[5] = {};
     for (uint64_t i = 0; i < 5; ++i)
       if (4 * (e - 1) + i < s->w) std::memcpy(&w5[i], (const uint8_t*)s->payload + 4 * (4 * (e - 1) + i), 4);
@@ -3107,7 +3144,7 @@ extern "C" int gh_ctx_load_device(gh_ctx* c, const gh_stream* s, uint64_t b, uin
     c->first_start = (wv >> (4 * (nib & 7))) & 15u;
   }
   c->ms_last_end = 0;
-  if ((c->ms || c->ws) && e == s->g) {
+  if ((c->ms || c->ws || c->wt) && e == s->g) {
     uint32_t w5[5] = {};
     const uint64_t lw0 = 4 * (c->nseg - 1);  // local word of the last segment
     const uint64_t nw = std::min<uint64_t>(5, have > lw0 ? have - lw0 : 0);
@@ -3285,6 +3322,10 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     t.lut = c->d_lut_t;
     t.out = c->d_out;
     t.agg = (unsigned int*)c->d_gran;
+    t.lutc = c->d_ws_lut_c;
+    t.kcbits = c->ws_kc;
+    t.lutc_bytes = 4u << c->ws_kc;
+    t.last_end = c->ms_last_end;
     t.status = c->d_misc + 1;
     t.total = (unsigned long long*)(c->d_misc + 2);
     t.junk = c->d_tile_junk;
@@ -3304,8 +3345,8 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     static thread_local WtParams tp;
     tp = t;
     ta[0] = &tp;
-    GH_HIP(hipLaunchKernel(wt_kernel_for(c->tile_g, c->grid - 1 > (uint32_t)WT_TB ? 2 : 1), dim3(c->grid),
-                           dim3(WT_TB), ta, c->lds, st));
+    GH_HIP(hipLaunchKernel(wt_kernel_for(c->tile_g, c->ws_kc, wt_ns(c->tables.maxsyms_seg), wt_lpw(c->grid)),
+                           dim3(c->grid), dim3(WT_TB), ta, c->lds, st));
     GH_HIP(hipEventRecord(dc.last, st));
     dc.has = true;
   } else if (c->tile) {

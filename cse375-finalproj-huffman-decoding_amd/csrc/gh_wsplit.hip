@@ -309,7 +309,8 @@ __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
   uint32_t hs = (uint32_t)(goff & 15);
   const unsigned long long rs = goff;  // the range's first output byte
   uint4* junk = p.junk + ((unsigned long long)(blockIdx.x * (uint32_t)NWAVE + (uint32_t)wid) * 64u + lane);
-  for (uint32_t blk = b0; blk < b1; ++blk) {
+  bool capped = false;  // the output ended at out_cap inside an earlier piece: nothing more to write
+  for (uint32_t blk = b0; blk < b1 && !capped; ++blk) {
     {
       int start[U];
       uint32_t cc[U];
@@ -343,7 +344,7 @@ __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
       }
       // a block that does not fit the wave's staging is staged one chain at a time
       const uint32_t nh = btot + 64u <= p.stage_bytes ? 1u : (uint32_t)U;
-      for (uint32_t h = 0; h < nh; ++h) {
+      for (uint32_t h = 0; h < nh && !capped; ++h) {
         const uint32_t hbytes = nh == 1 ? btot : ctot[h];
         const uint32_t lb = (uint32_t)(goff & 15);
         // staging byte 16 + lb + i = byte i of this half: staging chunk c <-> output
@@ -426,6 +427,15 @@ __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
             if (!(GH_WS_ABLATE & 2) && WS_CK(a0 + 16ull * c <= p.chk_out || !GH_WS_CHECK, 0x4000))
               *(uint4*)(p.out + a0 - 16 + 16ull * c) = st4[c];
         }
+        if (goff + hbytes >= p.out_cap) {
+          // the output ends in this piece: its partial last chunk (staging chunk cend,
+          // output bytes [out_cap & ~15, out_cap)) now, and no later piece writes
+          const uint32_t te = (uint32_t)(p.out_cap & 15);
+          if (te != 0 && p.out_cap > rs && !(GH_WS_ABLATE & 2) && WS_CK(p.out_cap <= p.chk_out || !GH_WS_CHECK, 0x8000))
+            ws_store_bytes(p.out + (p.out_cap - te), st4 + cend, cend == 1 ? hs : 0u, te, lane);
+          capped = true;
+          break;
+        }
         // carry the partial chunk cend to chunk 1 (the next piece's first output chunk;
         // bytes past the piece's end are that piece's first symbols, decoded here by the
         // last lookups, the same values it ORs in) and zero the rest, spill included
@@ -438,7 +448,7 @@ __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
     }
   }
   // the range's last, partial chunk: its bytes [hs or 0, end & 15), end clamped at out_cap
-  if (b0 < b1) {
+  if (b0 < b1 && !capped) {
     const unsigned long long ge = min(goff, p.out_cap);
     const uint32_t te = (uint32_t)(ge & 15);
     if (te != 0 && ge > rs && !(GH_WS_ABLATE & 2) && WS_CK(ge <= p.chk_out || !GH_WS_CHECK, 0x8000))

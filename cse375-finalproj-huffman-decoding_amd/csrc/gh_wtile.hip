@@ -1,35 +1,38 @@
 // Wave-tile decode ("wtile"), included by gh_decode.hip after the tile kernel (whose
-// e-window decode, aligned staging and fixed-count copy-out helpers it uses).
+// e-window decode, aligned staging and fixed-count copy-out helpers it uses) and after
+// gh_msplit.hip (count-LUT helpers).
 //
-// One persistent kernel, one decode pass, and no workgroup barrier after the LUT copy.
-// The unit of work is a wave tile: 64 x U consecutive segments (lane l owns segments
-// 64u + l of the tile).  A workgroup of NW waves takes NW consecutive wave tiles per
-// iteration (one "WG tile"); workgroup b takes WG tiles b, b + G, b + 2G, ... (static
-// round robin over the G resident workgroups), so iteration k of every workgroup is
-// round k.  Per iteration, each wave alone:
+// One persistent kernel, no workgroup barrier after the LUT copy, and no wave waiting
+// on another's prefix in steady state.  The unit of work is a wave tile: 64 x U
+// consecutive segments (lane l owns segments 64u + l of the tile).  A workgroup of NW
+// waves takes NW consecutive wave tiles per iteration (one "WG tile"); workgroup b takes
+// WG tiles b, b + G, b + 2G, ... (static round robin over the G resident workgroups).
 //
-//   1. decodes its tile from registers (words loaded one iteration earlier) into
-//      per-lane symbol words (single-symbol LUT on pre-shifted windows, grouped
-//      window shifts: decode_tile_grouped);
-//   2. scans the segment counts with DPP, writes its total to an LDS ring slot and
-//      bumps the slot's arrival counter; the wave that arrives last sums the NW
-//      totals and publishes the WG tile's aggregate granule (no wave waits here);
-//   3. (one wave per round) leads round k-1: loads the G aggregates of that round,
-//      scans them and publishes each WG tile's within-round prefix and the next
-//      round's offset R[k] = R[k-1] + round total;
-//   4. copies its tile of iteration k-2 out of its own LDS staging buffer with
-//      16-byte stores, at R[k-2] + the WG tile's prefix + the totals of the earlier
-//      waves of the WG tile (LDS ring, iteration k-2); the next tile's words are
-//      loaded just before those stores (fixed store count: vmcnt(N), not vmcnt(0));
-//   5. stages this tile into the buffer just emptied: aligned dwords, then the head
-//      bytes of each segment — one wave's LDS operations complete in order, so the
-//      two phases need no barrier.
+// The reference counts a tile, scans, and decodes it again (decoder.cu:529-728).  Here
+// the count runs WT_L iterations AHEAD of the decode, so a tile's aggregate is
+// published long before anyone needs it, and a tile is written out as soon as it is
+// decoded (one staging buffer per wave, no lag to cover).  In iteration k each wave:
 //
-// Every hand-off has an iteration of slack; a wave waits only when a prefix two
-// rounds old is still missing.  Reference counterpart: gpu_dec_l1_l2
-// (decoder.cu:454-730): count (:529-569), scan + decoupled look-back (:571-653),
-// decode and write (:655-728); its atomic ticket (:494-499) is a static round robin
-// here (a waiting wave never holds an unstarted tile of an earlier round).
+//   1. counts its wave tile of iteration k + L (words loaded one iteration earlier):
+//      codeword ends per segment with the wave split's end-mask LUT (one v_bcnt per
+//      lookup of up to 13 bits); the wave total goes to an LDS ring slot, and the last
+//      of the NW waves to arrive publishes the WG tile's aggregate (u32, epoch-tagged);
+//   2. sums its share of the G - 1 aggregates between the workgroup's tiles of
+//      iterations k and k+1 (loaded at the top of the iteration; published L - 1
+//      iterations ago), and the last arriver writes the WG tile prefix
+//         P(k+1) = P(k) + T(k) + sum
+//      to the LDS ring (P(k), T(k): the same workgroup's previous tile);
+//   3. decodes its wave tile of iteration k (single-symbol LUT on pre-shifted windows,
+//      grouped window shifts: decode_tile_grouped), scans the segment counts with DPP,
+//      stages the bytes in its LDS buffer (aligned dwords, then each segment's head
+//      bytes: one wave's LDS operations complete in order, so no barrier) and copies
+//      them out with 16-byte stores at P(k) + the earlier waves' counted totals.
+//
+// A workgroup waits only when another workgroup's count is L - 1 iterations behind.
+// The decode re-reads the payload the count read L iterations earlier: L x G x 32 KiB
+// of traffic lies between, far inside the 256 MiB Infinity Cache, so HBM sees the
+// payload once.  Reference counterpart: gpu_dec_l1_l2 (decoder.cu:454-730) — count
+// (:529-569), scan + decoupled look-back (:571-653), decode and write (:655-728).
 
 #ifndef GH_WT_DEFAULT
 #define GH_WT_DEFAULT 0  // wave-tile kernel by default for grouped codes (else the tile kernel)
@@ -40,33 +43,39 @@
 constexpr int WT_NW = GH_WT_NW;
 constexpr int WT_TB = 64 * WT_NW;
 constexpr int WT_U = 2;           // segments per lane per tile
-constexpr int WT_RING = 8;        // iterations of wave totals kept in LDS (see the ring note)
-#ifndef GH_WT_PF
-#define GH_WT_PF 2                // iterations between a tile's loads and its decode (1 or 2)
+constexpr int WT_RING = 16;       // LDS ring slots (iterations)
+#ifndef GH_WT_L
+#define GH_WT_L 2                 // iterations the count runs ahead of the decode (>= 1, <= 4)
 #endif
-constexpr uint32_t WT_PF = GH_WT_PF;
-#ifndef GH_WT_NS
-#define GH_WT_NS 2                // 16-byte stores per lane per copy-out (the rest loops)
-#endif
+constexpr int WT_L = GH_WT_L;
 #ifndef GH_WT_ABLATE
-#define GH_WT_ABLATE 0  // diagnostic variants only (results wrong): 1 no copy-out, 2 no prefix wait, 4 no staging, 8 no decode
+#define GH_WT_ABLATE 0  // diagnostic variants only (results wrong): 1 no copy-out, 4 no staging, 8 no decode, 16 no count
+#endif
+#ifndef GH_WT_PRIO
+#define GH_WT_PRIO 0  // alternate s_setprio between the two workgroup slots of a CU
+#endif
+#ifndef GH_WT_SCOPE
+#define GH_WT_SCOPE __HIP_MEMORY_SCOPE_AGENT  // scope of the aggregate stores and loads
 #endif
 constexpr unsigned long long WT_SPIN_TICKS = 400000000ull;  // 4 s of the 100 MHz clock
 
 #ifdef GH_STAMPS
 #define WT_STAMP_DECL unsigned long long wst_acc[8] = {}; unsigned long long wst_last = __builtin_amdgcn_s_memtime();
 #define WT_STAMP(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); wst_acc[i] += t_ - wst_last; wst_last = t_; } while (0)
+#define WT_COUNT(i) do { wst_acc[i] += 1; } while (0)
 #define WT_STAMP_FLUSH do { if (lane == 0 && p.stamps) { for (int i_ = 0; i_ < 8; ++i_) p.stamps[((size_t)blockIdx.x * NW + wid) * 16 + i_] = wst_acc[i_]; } } while (0)
 #else
 #define WT_STAMP_DECL
 #define WT_STAMP(i) do {} while (0)
+#define WT_COUNT(i) do {} while (0)
 #define WT_STAMP_FLUSH do {} while (0)
 #endif
 
 struct WtParams {
   const uint32_t* payload;       // local segment j owns words [4j, 4j+4); +1 look-ahead, zero padded
-  const uint32_t* gaps;          // nibble gap_nib0 + j - 1 = start of local segment j >= 1
-  const uint32_t* lut;           // 2^K u32 {len | sym << 24}
+  const uint32_t* gaps;          // nibble gap_nib0 + j - 1 = start of local segment j >= 1; + j its end
+  const uint32_t* lut;           // decode: 2^K u32 {len | sym << 24}
+  const uint32_t* lutc;          // count: 2^Kc u32 {b | end mask << 16}
   uint8_t* out;
   unsigned int* agg;             // per WG tile: epoch << 16 | its symbol count (<= 32768)
   unsigned int* status;
@@ -74,19 +83,38 @@ struct WtParams {
   uint4* junk;                   // 16 bytes per thread of the grid: padding stores with nothing to duplicate
   unsigned long long out_cap;
   unsigned int nseg, ntiles, ntw;  // segments, WG tiles, wave tiles with segments
-  unsigned int gap_nib0, first_start, kbits, lgr;
-  unsigned int epoch;            // 1 .. 0xFFFF (granules carry it in their high half)
-  unsigned int lut_bytes;        // LUT bytes in LDS (replicated 4 << (K + lgr))
-  unsigned int stage_bytes;      // one staging buffer of one wave
+  unsigned int gap_nib0, first_start, kbits, kcbits, lgr;
+  unsigned int last_end;         // != 0: end bit of local segment nseg-1 (the stream's last)
+  unsigned int epoch;            // 1 .. 0xFFFF (aggregates carry it in their high half)
+  unsigned int lut_bytes;        // decode LUT bytes in LDS (replicated 4 << (K + lgr))
+  unsigned int lutc_bytes;       // count LUT bytes in LDS (4 << Kc)
+  unsigned int stage_bytes;      // one wave's staging buffer
   unsigned long long* stamps;    // diagnostic build only (GH_STAMPS): per-wave phase cycles
 };
 
-// LDS after the LUT and the staging: per ring slot (iteration mod WT_RING) the NW wave
-// totals, the NW partial window sums, the WG tile's prefix (u64 as two words) and its
+// LDS after the two LUTs and the staging: per ring slot (iteration mod WT_RING) the NW
+// counted wave totals, the NW partial window sums, the WG tile's prefix (two words), its
 // tag, and two arrival counters.
 template <int NW>
-inline size_t wt_lds_bytes(size_t lut_bytes, size_t stage_bytes) {
-  return lut_bytes + (size_t)NW * 2 * stage_bytes + 4 * WT_RING * (2 * NW + 5) + 16;
+inline size_t wt_lds_bytes(size_t lut_bytes, size_t lutc_bytes, size_t stage_bytes) {
+  return lut_bytes + lutc_bytes + (size_t)NW * stage_bytes + 4 * WT_RING * (2 * NW + 5) + 16;
+}
+
+// LDS ring accesses at absolute LDS byte addresses (the kernel's LDS starts at 0).  Inline
+// asm: through a volatile generic pointer the compiler emits flat accesses, each followed
+// by vmcnt(0) — a wait for every outstanding global load and store of the wave.
+__device__ __forceinline__ uint32_t wt_ld(uint32_t a) {
+  uint32_t v;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+  return v;
+}
+__device__ __forceinline__ void wt_st(uint32_t a, uint32_t v) {
+  asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+__device__ __forceinline__ uint32_t wt_add(uint32_t a, uint32_t v) {
+  uint32_t r;
+  asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(a), "v"(v) : "memory");
+  return r;
 }
 
 __device__ __forceinline__ bool wt_ok(const WtParams& p, uint32_t v) { return (v >> 16) == p.epoch; }
@@ -99,7 +127,7 @@ __device__ __forceinline__ uint32_t wt_poll(const WtParams& p, unsigned int* g) 
     return p.epoch << 16;
   const unsigned long long t0 = wall_clock64();
   for (;;) {
-    const uint32_t v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t v = __hip_atomic_load(g, __ATOMIC_RELAXED, GH_WT_SCOPE);
     if (wt_ok(p, v)) return v;
     if (wall_clock64() - t0 > WT_SPIN_TICKS) {
       atomicOr(p.status, (unsigned)GH_ST_TIMEOUT);
@@ -109,39 +137,35 @@ __device__ __forceinline__ uint32_t wt_poll(const WtParams& p, unsigned int* g) 
   }
 }
 
-// Prefixes without a leader.  WG tile j = kG + b (iteration k of workgroup b) starts at
-//   P(j) = P(j - G) + T(j - G) + sum of the aggregates of WG tiles (j - G, j)
-// (P(j - G), T(j - G): the same workgroup's previous tile, held in LDS).  At the top of
-// iteration k every wave loads its share of the G - 1 aggregates for P of iteration
-// k-1 (one u32 per lane, published during iterations k-2 and k-1); after its decode it
-// sums them with DPP, and the last of the NW waves to arrive adds the partial sums and
-// writes P(k-1) to the LDS ring.  The copy-out of iteration k+1 reads it there.  No
-// workgroup waits on another's prefix, only on other workgroups' aggregates, which
-// are published right after each decode.
-//
-// LDS ring slots are reused every WT_RING iterations: waves of a workgroup stay within
-// two iterations of each other (a wave's copy-out of iteration k needs P(k-2), written
-// once every wave has finished the window step of iteration k-1), so 8 slots are ample.
-template <int NW, int GRP, int NS, int LPW>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4, 4)))
+// Ring slots are reused every WT_RING iterations.  The waves of a workgroup stay within
+// about one iteration of each other (a wave's copy-out of iteration k needs P(k), written
+// once every wave has finished the window step of iteration k-1), and a slot is last
+// read L + 1 iterations after it is written, so 8 slots suffice for L <= 4.
+// NS: 16-byte stores per lane per copy-out, enough for the worst-case wave tile (the
+// host picks 4 or 5 from the code's shortest codeword), so the store count is fixed.
+template <int NW, int GRP, int GC, int NS, int LPW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4, 8)))
 void gh_wtile_kernel(const WtParams p) {
   constexpr int U = WT_U;
   constexpr int TBW = 64 * NW;
   constexpr uint32_t R = WT_RING;
+  constexpr int L = WT_L;
+  static_assert(L >= 1 && L + 3 <= (int)R, "ring too small for the count-ahead distance");
+  static_assert(NW * 64 * U * 32 <= 65535, "WG tile total must fit the aggregate's 16 bits");
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  uint32_t* ring = (uint32_t*)(smem + p.lut_bytes + (size_t)NW * 2 * p.stage_bytes);
-  volatile uint32_t* s_wt = ring;                   // [R][NW] wave totals
-  volatile uint32_t* s_ps = ring + R * NW;          // [R][NW] partial window sums
-  volatile uint32_t* s_pk = ring + 2 * R * NW;      // [R][2] WG tile prefix (lo, hi)
-  volatile uint32_t* s_tag = ring + 2 * R * NW + 2 * R;  // [R] iteration whose prefix the slot holds
-  uint32_t* s_arr = ring + 2 * R * NW + 3 * R;      // [2][R] arrival counters (totals, windows)
-  {  // LUT to LDS, replicated: dword i of LDS = entry i >> lgr
-    const uint32_t nd = p.lut_bytes >> 2;
+  // ring (absolute LDS byte addresses): counted wave totals [R][NW], partial window sums
+  // [R][NW], WG tile prefixes [R][2] (lo, hi), tags [R], arrival counters [2][R]
+  const uint32_t a_ct = p.lut_bytes + p.lutc_bytes + (uint32_t)NW * p.stage_bytes;
+  const uint32_t a_ps = a_ct + 4u * R * NW, a_pk = a_ps + 4u * R * NW, a_tag = a_pk + 8u * R,
+                 a_arr = a_tag + 4u * R;
+  {  // LUTs to LDS: decode replicated (dword i = entry i >> lgr), count as is
     uint32_t* sl = (uint32_t*)smem;
-    for (uint32_t i = tid; i < nd; i += TBW) sl[i] = p.lut[i >> p.lgr];
-    if (tid < (int)R) s_tag[tid] = 0xFFFFFFFFu;
-    if (tid < 2 * (int)R) s_arr[tid] = 0;
+    for (uint32_t i = tid; i < (p.lut_bytes >> 2); i += TBW) sl[i] = p.lut[i >> p.lgr];
+    uint32_t* sc = (uint32_t*)(smem + p.lut_bytes);
+    for (uint32_t i = tid; i < (p.lutc_bytes >> 2); i += TBW) sc[i] = p.lutc[i];
+    if (tid < (int)R) wt_st(a_tag + 4u * tid, 0xFFFFFFFFu);
+    if (tid < 2 * (int)R) wt_st(a_arr + 4u * tid, 0u);
   }
   if (tid == 0 && (uint32_t)(size_t)(const __attribute__((address_space(3))) uint8_t*)smem != 0u)
     atomicOr(p.status, (unsigned)GH_ST_LAYOUT);
@@ -150,20 +174,38 @@ void gh_wtile_kernel(const WtParams p) {
   const uint32_t S = 30u - p.kbits - p.lgr;
   const uint32_t amask = ((1u << p.kbits) - 1u) << (2u + p.lgr);
   const uint32_t laneoff = ((uint32_t)lane & ((1u << p.lgr) - 1u)) << 2;
-  const uint32_t G = gridDim.x, vb = blockIdx.x;  // host: G <= ntiles, G - 1 <= 64 * NW * LPW
-  const uint32_t last_k = (p.ntiles - 1u - vb) / G;
-  const uint32_t stg0 = p.lut_bytes + (uint32_t)wid * 2u * p.stage_bytes;  // absolute LDS address
+  const uint32_t csh = 30u - p.kcbits;                   // count LUT: index bits -> byte offset
+  const uint32_t cmask = ((1u << p.kcbits) - 1u) << 2;
+  const uint32_t cbase = p.lut_bytes;                    // absolute LDS address of the count LUT
+  const uint32_t G = gridDim.x, vb = blockIdx.x;         // host: G <= ntiles, G - 1 <= 64 * NW * LPW
+  const int last_k = (int)((p.ntiles - 1u - vb) / G);
+  const uint32_t buf = p.lut_bytes + p.lutc_bytes + (uint32_t)wid * p.stage_bytes;  // absolute LDS address
   uint4* junk = p.junk + (size_t)blockIdx.x * TBW + tid;
   const uint32_t ezero = p.epoch << 16;
+  auto wave_tile = [&](int k) { return min((uint32_t)k * G + vb, p.ntiles - 1u) * (uint32_t)NW + (uint32_t)wid; };
 
-  // a tile's words: loaded WT_PF iterations before its decode (register sets A, B)
-  struct Words {
+  // a tile's words and gap words; loaded one iteration before they are used
+  struct CWords {  // count pass: start and end nibbles
+    uint4 w[U];
+    uint32_t w4[U], ga[U], gb[U];
+  };
+  struct DWords {  // decode pass: start nibble
     uint4 w[U];
     uint32_t w4[U], gw[U];
   };
-  auto load = [&](uint32_t k, Words& r) {
-    const uint32_t t = min(k * G + vb, p.ntiles - 1u) * (uint32_t)NW + (uint32_t)wid;  // wave tile
-    const uint32_t seg0 = t * (uint32_t)(64 * U) + (uint32_t)lane;
+  auto load_c = [&](int k, CWords& r) {
+    const uint32_t seg0 = wave_tile(k) * (uint32_t)(64 * U) + (uint32_t)lane;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t sc = min(seg0 + (uint32_t)(64 * u), p.nseg - 1u);
+      r.w[u] = *(const uint4*)(p.payload + 4ull * sc);
+      r.w4[u] = p.payload[4ull * sc + 4];
+      r.ga[u] = p.gaps[(p.gap_nib0 + (sc ? sc - 1u : 0u)) >> 3];
+      r.gb[u] = p.gaps[(p.gap_nib0 + sc) >> 3];
+    }
+  };
+  auto load_d = [&](int k, DWords& r) {
+    const uint32_t seg0 = wave_tile(k) * (uint32_t)(64 * U) + (uint32_t)lane;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t sc = min(seg0 + (uint32_t)(64 * u), p.nseg - 1u);
@@ -172,25 +214,176 @@ void gh_wtile_kernel(const WtParams p) {
       r.gw[u] = p.gaps[(p.gap_nib0 + (sc ? sc - 1u : 0u)) >> 3];
     }
   };
-  uint32_t tot1 = 0, tot2 = 0;  // this wave's totals of iterations k-1, k-2
+  // Every iteration issues the same global operations, unconditionally (clamped
+  // addresses, stores to junk slots when there is nothing to write): one window load,
+  // the next count tile's loads, one aggregate store, the next decode tile's loads and
+  // NS + 1 copy-out stores.  Loads and stores share the in-order vmcnt counter, so a
+  // fixed sequence lets the compiler wait for a prefetch with vmcnt(N) instead of
+  // vmcnt(0) (which would wait for every store still in flight).
+  uint32_t* const agg_junk = (uint32_t*)junk;
+  uint32_t bad = 0;                 // counted and decoded totals differ (corrupted stream)
+  unsigned long long total = ~0ull;  // lane 0 of the wave holding the last wave tile
+  // two register sets each, alternating by iteration parity (the loop is unrolled by
+  // two), so a prefetch lands in the registers its consumer reads: no copies at the
+  // loop's back edge, whose moves would each wait for the load in flight
+  CWords cwA, cwB;
+  DWords dwA, dwB;
+  load_c(0, cwA);
+  load_d(-L, dwA);
   WT_STAMP_DECL
-  auto iter = [&](uint32_t k, Words& cur) {
-    const bool have_cur = k <= last_k;
-    const bool have2 = k >= 2;
-    const uint32_t j = k * G + vb;                        // WG tile of this iteration
-    const uint32_t t = j * (uint32_t)NW + (uint32_t)wid;  // wave tile
-    const uint32_t slot = k % R;
-    // window of P(k-1): WG tiles [lo, jp), jp = (k-1)G + b
-    const bool do_pref = k >= 1 && k - 1u <= last_k;
-    const uint32_t jp = j - G, lo = jp >= G ? jp - G + 1u : 0u;
+  // count of iteration k + L, the window of P(k + 1)
+  auto count_step = [&](int k, CWords& cw, CWords& cwn) {
+#if GH_WT_PRIO
+    // the second workgroup dispatched to a CU loses every issue-arbitration tie to the
+    // first (age order): alternate the two slots' priority by iteration
+    if ((((uint32_t)(k + 64) + (vb >= (G >> 1) ? 1u : 0u)) & 1u) != 0u) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+#endif
+    const bool do_pref = k + 1 >= 0 && k + 1 <= last_k;
+    const uint32_t jn = (uint32_t)(k + 1) * G + vb, lo = jn >= G ? jn - G + 1u : 0u;
     uint32_t wv[LPW];
 #pragma unroll
     for (int q = 0; q < LPW; ++q) {
       const uint32_t i = lo + (uint32_t)((q * NW + wid) * 64 + lane);
-      wv[q] = (do_pref && i < jp) ? __hip_atomic_load(&p.agg[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                  : ezero;
+      const uint32_t v = __hip_atomic_load(&p.agg[do_pref && i < jn ? i : 0u], __ATOMIC_RELAXED, GH_WT_SCOPE);
+      wv[q] = (do_pref && i < jn) ? v : ezero;
     }
-    // ---- 1. decode ------------------------------------------------------------
+    const int kc = k + L;
+    const bool have_c = kc <= last_k;
+    const uint32_t seg0 = wave_tile(kc) * (uint32_t)(64 * U) + (uint32_t)lane;
+    Win v[U];
+    int Rb[U];
+    uint32_t cnt[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t seg = seg0 + (uint32_t)(64 * u);
+      const bool act = have_c && seg < p.nseg;
+      const int start = seg == 0 ? (int)p.first_start : (int)ms_nib(cw.ga[u], p.gap_nib0 + seg - 1u);
+      const int E = (p.last_end && seg == p.nseg - 1u) ? (int)p.last_end
+                                                       : 128 + (int)ms_nib(cw.gb[u], p.gap_nib0 + seg);
+      v[u] = make_win(cw.w[u], cw.w4[u], start);
+      Rb[u] = act ? E - start : 0;
+      cnt[u] = 0;
+    }
+    load_c(kc + 1, cwn);  // the next count tile's words (clamped; always issued)
+    if (!(GH_WT_ABLATE & 16)) {
+      for (int g = 0; g < 160; ++g) {
+        uint32_t rm[U], q[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          rm[u] = ms_rmask(Rb[u]);
+          q[u] = 32u;
+        }
+#pragma unroll
+        for (int j = 0; j < GC; ++j) {
+          uint32_t e[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const uint32_t x = j == 0 ? v[u].d0 : __builtin_amdgcn_alignbit(v[u].d0, v[u].d1, q[u]);
+            asm volatile("ds_read_b32 %0, %1" : "=v"(e[u]) : "v"(((x >> csh) & cmask) + cbase) : "memory");
+          }
+          lds_wait_all(e);
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            uint32_t m;
+            asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD"
+                : "=v"(m) : "v"(e[u]), "v"(rm[u]));
+            cnt[u] = __builtin_popcount(m) + cnt[u];
+            asm("v_ashrrev_i32 %0, %1, %0" : "+v"(rm[u]) : "v"(e[u]));
+            q[u] -= e[u];
+          }
+        }
+        bool more = false;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          ms_shift(v[u], q[u]);  // consumed = 32 - (q & 0xFFFF): v_alignbit reads q & 31
+          Rb[u] -= 32 - (int)(q[u] & 0xFFFFu);
+          more |= Rb[u] > 0;
+        }
+        if (!__any(more)) break;
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) cnt[u] = Rb[u] > 0 ? 16u : 0u;
+    }
+    uint32_t ctot = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) ctot += cnt[u];
+    ctot = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(ctot, lane), 63);
+    // wave total to the ring; the last of the NW waves publishes the WG tile's aggregate
+    // (every wave stores: the others to their junk slot)
+    uint32_t* adst = agg_junk;
+    uint32_t aval = 0;
+    if (lane == 0 && have_c) {
+      const uint32_t slot = (uint32_t)kc % R;
+      wt_st(a_ct + 4u * (slot * NW + wid), ctot);
+      const uint32_t old = wt_add(a_arr + 4u * slot, 1u);
+      if (old % NW == NW - 1) {
+#pragma unroll
+        for (int q = 0; q < NW; ++q) aval += wt_ld(a_ct + 4u * (slot * NW + q));
+        aval |= ezero;
+        adst = &p.agg[(uint32_t)kc * G + vb];
+      }
+    }
+    __hip_atomic_store(lane == 0 ? adst : agg_junk, aval, __ATOMIC_RELAXED, GH_WT_SCOPE);
+    WT_STAMP(0);
+    // window sum; the last arriver writes P(k+1) to the ring
+    if (do_pref) {
+      bool ready = true;
+#pragma unroll
+      for (int q = 0; q < LPW; ++q) ready &= wt_ok(p, wv[q]);
+      if (!__all(ready)) {
+        WT_COUNT(6);
+#ifdef GH_STAMPS
+        // diagnostics: poll rounds (one sc1 load each) until every window value is fresh
+        for (int rounds = 0; rounds < 100000; ++rounds) {
+          bool all = true;
+#pragma unroll
+          for (int q = 0; q < LPW; ++q)
+            if (!wt_ok(p, wv[q])) {
+              wv[q] = __hip_atomic_load(&p.agg[lo + (uint32_t)((q * NW + wid) * 64 + lane)], __ATOMIC_RELAXED,
+                                        GH_WT_SCOPE);
+              all = false;
+            }
+          if (__all(all)) break;
+          WT_COUNT(7);
+        }
+#else
+#pragma unroll
+        for (int q = 0; q < LPW; ++q)
+          if (!wt_ok(p, wv[q])) wv[q] = wt_poll(p, &p.agg[lo + (uint32_t)((q * NW + wid) * 64 + lane)]);
+#endif
+      }
+      uint32_t ws = 0;
+#pragma unroll
+      for (int q = 0; q < LPW; ++q) ws += wv[q] & 0xFFFFu;
+      ws = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(ws, lane), 63);  // < 2^32
+      if (lane == 0) {
+        const uint32_t slot = (uint32_t)(k + 1) % R;
+        wt_st(a_ps + 4u * (slot * NW + wid), ws);
+        const uint32_t old = wt_add(a_arr + 4u * (R + slot), 1u);
+        if (old % NW == NW - 1) {
+          unsigned long long pk = 0;
+          if (k >= 0) {  // P(k) + T(k)
+            const uint32_t s0 = (uint32_t)k % R;
+            pk = ((unsigned long long)wt_ld(a_pk + 8u * s0 + 4u) << 32) | wt_ld(a_pk + 8u * s0);
+#pragma unroll
+            for (int q = 0; q < NW; ++q) pk += wt_ld(a_ct + 4u * (s0 * NW + q));
+          }
+#pragma unroll
+          for (int q = 0; q < NW; ++q) pk += wt_ld(a_ps + 4u * (slot * NW + q));
+          wt_st(a_pk + 8u * slot, (uint32_t)pk);
+          wt_st(a_pk + 8u * slot + 4u, (uint32_t)(pk >> 32));
+          wt_st(a_tag + 4u * slot, (uint32_t)(k + 1));  // after the value: one wave's LDS ops complete in order
+        }
+      }
+    }
+    WT_STAMP(1);
+  };
+  // decode, stage and copy out the wave tile of iteration k
+  auto decode_step = [&](int k, DWords& dw, DWords& dwn) {
+    const bool have_d = k >= 0;
+    const uint32_t t = wave_tile(k < 0 ? 0 : k);
     uint32_t ow[U][OW], cnt[U];
     {
       int start[U];
@@ -200,32 +393,25 @@ void gh_wtile_kernel(const WtParams p) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const uint32_t seg = seg0 + (uint32_t)(64 * u);
-        act[u] = have_cur && seg < p.nseg;
+        act[u] = have_d && seg < p.nseg;
         const uint32_t nib = (p.gap_nib0 + seg - 1u) & 7u;
-        start[u] = seg == 0 ? (int)p.first_start : (int)((cur.gw[u] >> (4 * nib)) & 15u);
-        make_ewin(cur.w[u], cur.w4[u], start[u], S, e[u]);
+        start[u] = seg == 0 ? (int)p.first_start : (int)((dw.gw[u] >> (4 * nib)) & 15u);
+        make_ewin(dw.w[u], dw.w4[u], start[u], S, e[u]);
       }
+      load_d(k + 1, dwn);  // the next decode tile's words (clamped; the count read them: cache hits)
       auto nothing = [&]() {};
-      if (have_cur && (GH_WT_ABLATE & 8)) {
+      if (GH_WT_ABLATE & 8) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           cnt[u] = act[u] ? 16u : 0u;
 #pragma unroll
           for (int m = 0; m < OW; ++m) ow[u][m] = m < 5 ? e[u][m] : 0u;
         }
-      } else if (have_cur) {
-        decode_tile_grouped<GRP, U, 1000>(e, start, act, ow, cnt, amask, laneoff, nothing);
       } else {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          cnt[u] = 0;
-#pragma unroll
-          for (int m = 0; m < OW; ++m) ow[u][m] = 0;
-        }
+        decode_tile_grouped<GRP, U, 1000>(e, start, act, ow, cnt, amask, laneoff, nothing);
       }
     }
-    WT_STAMP(0);
-    // ---- 2. scan; wave total to the LDS ring; the last arriver publishes -------
+    WT_STAMP(2);
     uint32_t lpos[U], wtot = 0;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -233,88 +419,29 @@ void gh_wtile_kernel(const WtParams p) {
       lpos[u] = wtot + incl - cnt[u];
       wtot += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     }
-    if (have_cur && lane == 0) {
-      s_wt[slot * NW + wid] = wtot;
-      const uint32_t old = __hip_atomic_fetch_add(&s_arr[slot], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (old % NW == NW - 1) {
-        uint32_t sum = 0;
-#pragma unroll
-        for (int q = 0; q < NW; ++q) sum += s_wt[slot * NW + q];
-        __hip_atomic_store(&p.agg[j], ezero | sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    WT_STAMP(1);
-    // ---- 3. window sum; the last arriver writes P(k-1) --------------------------
-    if (do_pref) {
-      bool ready = true;
-#pragma unroll
-      for (int q = 0; q < LPW; ++q) ready &= wt_ok(p, wv[q]);
-      if (!__all(ready)) {
-#pragma unroll
-        for (int q = 0; q < LPW; ++q)
-          if (!wt_ok(p, wv[q])) wv[q] = wt_poll(p, &p.agg[lo + (uint32_t)((q * NW + wid) * 64 + lane)]);
-      }
-      uint32_t ws = 0;
-#pragma unroll
-      for (int q = 0; q < LPW; ++q) ws += wv[q] & 0xFFFFu;
-      ws = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(ws, lane), 63);  // < 2^32
-      if (lane == 0) {
-        s_ps[slot * NW + wid] = ws;
-        const uint32_t old = __hip_atomic_fetch_add(&s_arr[R + slot], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (old % NW == NW - 1) {
-          unsigned long long pk = 0;
-          if (k >= 2) {
-            const uint32_t s2 = (k - 2u) % R;
-            pk = ((unsigned long long)s_pk[2 * s2 + 1] << 32) | s_pk[2 * s2];
-#pragma unroll
-            for (int q = 0; q < NW; ++q) pk += s_wt[s2 * NW + q];
+    unsigned long long goff = ~0ull;  // k < 0: past out_cap, nothing written
+    if (lane == 0 && have_d) {
+      const uint32_t s0 = (uint32_t)k % R;
+      if (wt_ld(a_tag + 4u * s0) != (uint32_t)k) {  // written once every wave did the window step of k-1
+        const unsigned long long t0 = wall_clock64();
+        while (wt_ld(a_tag + 4u * s0) != (uint32_t)k) {
+          if (wall_clock64() - t0 > WT_SPIN_TICKS) {
+            bad |= GH_ST_TIMEOUT;
+            break;
           }
-#pragma unroll
-          for (int q = 0; q < NW; ++q) pk += s_ps[slot * NW + q];
-          const uint32_t s1 = (k - 1u) % R;
-          s_pk[2 * s1] = (uint32_t)pk;
-          s_pk[2 * s1 + 1] = (uint32_t)(pk >> 32);
-          s_tag[s1] = k - 1u;
+          __builtin_amdgcn_s_sleep(1);
         }
       }
-    }
-    WT_STAMP(2);
-    // ---- 4. copy out the tile of iteration k-2 ---------------------------------
-    const uint32_t buf = stg0 + (k & 1u) * p.stage_bytes;
-    if (have2) {
-      unsigned long long goff = 0;
-      if ((GH_WT_ABLATE & 2) && lane == 0) {
-        goff = (unsigned long long)(j - 2u * G) * NW * 2048ull + wid * 2048ull;
-      } else if (lane == 0) {
-        const uint32_t s2 = (k - 2u) % R;
-        if (s_tag[s2] != k - 2u) {  // written once every wave of the WG did iteration k-1's window step
-          const unsigned long long t0 = wall_clock64();
-          while (s_tag[s2] != k - 2u) {
-            if (wall_clock64() - t0 > WT_SPIN_TICKS) {
-              atomicOr(p.status, (unsigned)GH_ST_TIMEOUT);
-              break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-          }
-        }
-        goff = ((unsigned long long)s_pk[2 * s2 + 1] << 32) | s_pk[2 * s2];
+      goff = ((unsigned long long)wt_ld(a_pk + 8u * s0 + 4u) << 32) | wt_ld(a_pk + 8u * s0);
 #pragma unroll
-        for (int q = 0; q < NW - 1; ++q)
-          if (q < wid) goff += s_wt[s2 * NW + q];
-        if ((j - 2u * G) * (uint32_t)NW + (uint32_t)wid == p.ntw - 1u) *p.total = goff + tot2;
-      }
-      goff = rfl_u64(goff);
-      WT_STAMP(3);
-      const uint32_t n2 =
-          goff >= p.out_cap ? 0u : (uint32_t)min<unsigned long long>(tot2, p.out_cap - goff);
-      if constexpr (WT_PF == 1) load(k + 1u, cur);  // the next tile's words, before this copy-out's stores
-      if (!(GH_WT_ABLATE & 1)) copy_out_tile_fixed<64, NS>(p.out, buf, goff, n2, lane, junk);
-    } else if constexpr (WT_PF == 1) {
-      load(k + 1u, cur);
+      for (int q = 0; q < NW - 1; ++q)
+        if (q < wid) goff += wt_ld(a_ct + 4u * (s0 * NW + q));
+      if (wt_ld(a_ct + 4u * (s0 * NW + wid)) != wtot) bad |= GH_ST_BADCODE;
+      if (t == p.ntw - 1u) total = goff + wtot;
     }
-    WT_STAMP(4);
-    // ---- 5. stage this tile (the buffer just emptied) ---------------------------
-    if (have_cur && !(GH_WT_ABLATE & 4)) {
+    goff = rfl_u64(goff);
+    WT_STAMP(3);
+    if (!(GH_WT_ABLATE & 4)) {
       const uint32_t sbase = buf + STAGE_PAD;
       uint32_t nb[U];
 #pragma unroll
@@ -323,24 +450,23 @@ void gh_wtile_kernel(const WtParams p) {
       for (int u = 0; u < U; ++u)
         if (nb[u]) stage_head(sbase + lpos[u], ow[u][0], nb[u]);
     }
+    WT_STAMP(4);
+    const uint32_t n = goff >= p.out_cap ? 0u : (uint32_t)min<unsigned long long>(wtot, p.out_cap - goff);
+    if (!(GH_WT_ABLATE & 1)) copy_out_tile_fixed<64, NS, false>(p.out, buf, goff, n, lane, junk);
     WT_STAMP(5);
-    // two iterations ahead: the tile after next, issued once this tile is staged (the
-    // other register set is in flight meanwhile)
-    if constexpr (WT_PF == 2) load(k + 2u, cur);
-    tot2 = tot1;
-    tot1 = wtot;
-    WT_STAMP(6);
   };
-  Words A, B;
-  load(0, A);
-  if constexpr (WT_PF == 1) {
-    for (uint32_t k = 0; k <= last_k + 2u; ++k) iter(k, A);
-  } else {
-    load(1, B);
-    for (uint32_t k = 0; k <= last_k + 2u; k += 2) {
-      iter(k, A);
-      if (k + 1u <= last_k + 2u) iter(k + 1u, B);
-    }
+  // One loop from k = -L: iterations k < 0 count only (their decode step runs on no
+  // segment and stores to junk slots), so every iteration issues the same operations.
+  for (int k = -L; k <= last_k; k += 2) {
+    count_step(k, cwA, cwB);
+    decode_step(k, dwA, dwB);
+    if (k + 1 > last_k) break;
+    count_step(k + 1, cwB, cwA);
+    decode_step(k + 1, dwB, dwA);
   }
+  // rare outcomes, reported once (a conditional atomic inside the loop would break the
+  // fixed operation sequence above)
+  if (lane == 0 && bad) atomicOr(p.status, bad);
+  if (lane == 0 && total != ~0ull) *p.total = total;
   WT_STAMP_FLUSH;
 }

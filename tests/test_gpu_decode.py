@@ -385,3 +385,28 @@ def test_wave_tile_repeated_shards_and_cap(gpu, orc, percu, monkeypatch):
             r = d.report()
             assert r.status == 0 and r.out_bytes == cap
             assert np.array_equal(d.download(cap), data[:cap])
+
+
+@pytest.mark.parametrize("mode,r", [("wsplit", 0.5), ("wsplit", 0.9), ("tile", 0.1), ("wtile", 0.1)])
+def test_output_capacity_below_total(gpu, mode, r, monkeypatch):
+    """An output capacity below the stream's total (gh_ctx_load out_cap) writes exactly
+    the prefix that fits: caps inside the first chunk, mid-range, at a range edge and
+    just below the end, on the default grid and (wave split) on 3 workgroups, whose
+    long ranges are staged in many pieces (a piece that crosses the cap must not be
+    followed by writes of later pieces)."""
+    monkeypatch.setenv("GH_MODE", mode)
+    data = gpu.generate(81, r, 2_000_003)
+    s = gpu.parse(gpu.encode(data))
+    for grid in (("", "3") if mode == "wsplit" else ("",)):
+        if grid:
+            monkeypatch.setenv("GH_WS_GRID", grid)
+        for cap in (1, 9, 16, 4099, 777_777, 1_999_990):
+            with gpu.Decoder(0) as d:
+                d.load(s, 0, s.g, out_cap=cap)
+                d.decode()
+                rep = d.report()
+                assert rep.status == 0 and rep.out_bytes == cap
+                got = d.download(cap)
+                if not np.array_equal(got, data[:cap]):
+                    bad = np.nonzero(got != data[:cap])[0]
+                    raise AssertionError(f"{mode} grid={grid} cap={cap}: {bad.size} wrong bytes, first at {bad[0]}")
