@@ -118,6 +118,16 @@ def cpu_baseline(r: float, seed: int, sample: int) -> dict:
         base = {"value": round(sample / dt / 1e9, 6), "unit": "GB/s", "cores": 1, "kind": "port",
                 "sample": f"{sample} B generate(r={r}, seed={seed}); oracle bit-serial decode, "
                           f"{dt:.3f} s, verified {bool(np.array_equal(dec, data))}"}
+        # BASELINE configs[0] literally: sequential.cpp on 10 MB of redundancy-0.5 data
+        try:
+            d1 = gh.generate(seed, 0.5, 10**7)
+            o = oracle.run_reference_cpu("sequential", d1)
+            extra.append({"program": "sequential", "config": "configs[0]: 10^7 B, redundancy 0.5",
+                          "threads": 1, "value": round(10**7 / (o["decode_us"] * 1e-6) / 1e9, 6),
+                          "unit": "GB/s", "decode_s": round(o["decode_us"] / 1e6, 4),
+                          "verified": o["verified"]})
+        except Exception as e:  # reported, not fatal
+            extra.append({"program": "sequential", "config": "configs[0]", "error": str(e)[:200]})
     if extra:
         base["others"] = extra
     base["host_cpus"] = nproc
@@ -156,6 +166,67 @@ def copy_yardstick(nbytes: int, stream: int, device) -> float:
     return 2 * half / (ms * 1e-3) / 1e9
 
 
+def end_to_end(img: np.ndarray, args, r: float, dev, threads: int) -> dict:
+    """File in, file out, never part of `value`: the compressed image is written to a
+    file (untimed), then timed: a fresh context streams it to HBM (gh_ctx_load_file),
+    decodes it and streams the output to a second file (gh_ctx_save_file).  Also timed
+    in the reference's own scope (decoder/src/huff.cpp:106-129: host buffer -> device,
+    decode, device -> host buffer; file reads and fwrite outside it).  The output file
+    is checked against the generator."""
+    import torch
+
+    s = gh.parse(img)
+    n = s.n
+    d = gh_dist.pick_share_dir(None, 0, int(img.size) + n, args.shm, dev)
+    src = os.path.join(d, f"gh_e2e_{os.getpid()}.huff")
+    dst = os.path.join(d, f"gh_e2e_{os.getpid()}.out")
+    res = {"dir": d}
+    try:
+        img.tofile(src)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with gh.Decoder(dev.index or 0) as d2:
+            d2.load_file(src)
+            t1 = time.perf_counter()
+            d2.decode()
+            rep = d2.report()
+            t2 = time.perf_counter()
+            d2.save_file(dst, n)
+            t3 = time.perf_counter()
+        res.update({"file_to_file_ms": round((t3 - t0) * 1e3, 2), "load_file_ms": round((t1 - t0) * 1e3, 2),
+                    "decode_ms": round((t2 - t1) * 1e3, 3), "save_file_ms": round((t3 - t2) * 1e3, 2),
+                    "file_to_file_gbps": round(n / (t3 - t0) / 1e9, 3), "status": int(rep.status)})
+        out = np.memmap(dst, dtype=np.uint8, mode="r")
+        ok = out.size == n
+        step = 1 << 27
+        for off in range(0, n, step):
+            if not ok:
+                break
+            ok = gh_dist.verify_slice(np.asarray(out[off:off + step]), args.seed, r, off, threads=threads)
+        del out
+        res["bitexact"] = bool(ok)
+        # the reference's scope: host image -> HBM, decode, HBM -> host buffer
+        host = np.empty(n, dtype=np.uint8)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with gh.Decoder(dev.index or 0) as d3:
+            d3.load(s)
+            d3.decode()
+            d3.report()
+            host[:] = d3.download(n)
+        res["ref_scope_ms"] = round((time.perf_counter() - t0) * 1e3, 2)
+        res["ref_scope_note"] = ("decoder_l1_l2 scope: context + H2D (pageable) + decode + D2H, "
+                                 "as the reference's 'Decode time' (huff.cpp:106-129)")
+        del host, s
+    finally:
+        for f in (src, dst):
+            try:
+                os.unlink(f)
+            except OSError:
+                pass
+    return res
+
+
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
@@ -169,7 +240,12 @@ def main() -> int:
     ap.add_argument("--threads", type=int, default=0, help="host threads for generate/encode (0 = auto)")
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the RCCL output gather")
     ap.add_argument("--no-copy", action="store_true", help="skip the streaming-copy yardstick")
-    ap.add_argument("--shm", default="/dev/shm", help="N>1: directory of the shared stream file")
+    ap.add_argument("--shm", default="/dev/shm", help="N>1: directory of the shared stream file "
+                    "(checked for free space; falls back to TMPDIR, /tmp or the working directory)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="run the multi-GPU path (torch.distributed over RCCL, shared stream file, "
+                         "per-rank file loading, offsets, RCCL gather) even at one rank")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end file-to-file timing")
     ap.add_argument("--out-json", default="", help="also write the JSON line to this file (rank 0)")
     args = ap.parse_args()
 
@@ -183,8 +259,13 @@ def main() -> int:
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
-    if world > 1:
+    use_dist = world > 1 or args.force_dist
+    if use_dist:
         import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group("nccl", device_id=dev)
     threads = args.threads or gh_dist.host_threads()
 
@@ -195,7 +276,9 @@ def main() -> int:
 
     t0 = time.time()
     dec = gh.Decoder(local)
-    if world == 1:
+    e2e_img = None  # N=1: the image, kept for the end-to-end timing
+    share_dir = None
+    if not use_dist:
         data = gh.generate(args.seed, r, total, threads=threads)
         img = gh.encode(data, threads=threads)
         del data
@@ -206,27 +289,37 @@ def main() -> int:
         dec.load(s)
         torch.cuda.synchronize()
         load_ms = (time.time() - t1) * 1e3
-        del img, s
+        del s
+        if not args.no_e2e:
+            e2e_img = img
+        del img
     else:
         port = os.environ.get("MASTER_PORT", "0")
-        path = os.path.join(args.shm, f"gh_bench_{port}_{args.workload}_{per_gpu}_{world}.huff")
+        # the stream file: about the input size (r >= 0 codes average <= 8.1 bits a byte)
+        share_dir = gh_dist.pick_share_dir(dist, rank, int(total * 1.05) + (1 << 20), args.shm, dev)
+        path = os.path.join(share_dir, f"gh_bench_{port}_{args.workload}_{per_gpu}_{world}.huff")
+        if rank == 0 and share_dir != args.shm:
+            log(f"[rank 0] {args.shm} lacks room for the stream: using {share_dir}")
 
         def make_image():
             d = gh.generate(args.seed, r, total, threads=threads)
             return gh.encode(d, threads=threads)
 
-        hdr = gh_dist.share_stream(dist, rank, path, make_image, dev)
-        b, e = gh_dist.shard_range(hdr["g"], world, rank)
-        t1 = time.time()
-        dec.load_file(path, b, e)
-        torch.cuda.synchronize()
-        load_ms = (time.time() - t1) * 1e3
-        dist.barrier()
-        if rank == 0:
-            try:
-                os.unlink(path)
-            except OSError:
-                pass
+        try:
+            hdr = gh_dist.share_stream(dist, rank, path, make_image, dev)
+            b, e = gh_dist.shard_range(hdr["g"], world, rank)
+            t1 = time.time()
+            dec.load_file(path, b, e)
+            torch.cuda.synchronize()
+            load_ms = (time.time() - t1) * 1e3
+            dist.barrier()
+        finally:  # never leave the stream in RAM-backed tmpfs, whatever failed
+            if rank == 0:
+                for f in (path, path + ".part"):
+                    try:
+                        os.unlink(f)
+                    except OSError:
+                        pass
     log(f"[rank {rank}] N={hdr['n']} W={hdr['w']} G={hdr['g']} v{hdr['version']} shard=[{b},{e}) "
         f"setup {t1 - t0:.1f}s load {load_ms:.1f} ms")
 
@@ -290,6 +383,14 @@ def main() -> int:
         except Exception as ex:  # the yardstick must not hide the decode number
             log(f"copy yardstick failed: {ex}")
 
+    e2e = None
+    if e2e_img is not None:
+        try:
+            e2e = end_to_end(e2e_img, args, r, dev, threads)
+        except Exception as ex:  # reported, never hides the decode number
+            e2e = {"error": str(ex)[:300]}
+        del e2e_img
+
     if rank == 0:
         achieved = alg / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
         read_bytes = alg - shard_bytes
@@ -331,10 +432,13 @@ def main() -> int:
             "gather_ms": None if gather_ms is None else round(gather_ms, 3),
             "gather_bitexact": gather_ok,
             "load_ms": round(load_ms, 2),
-            "load_kind": "host memory -> HBM (pageable)" if world == 1 else
-                         "gh_ctx_load_file: /dev/shm file -> pinned -> HBM, shard words only",
+            "load_kind": "host memory -> HBM (pageable)" if not use_dist else
+                         f"gh_ctx_load_file: {share_dir} file -> pinned -> HBM, shard words only",
+            "dist": {"backend": "nccl (RCCL)", "world": world, "forced": bool(args.force_dist and world == 1),
+                     "share_dir": share_dir} if use_dist else None,
+            "e2e": e2e,
         }
-        if world == 1 and args.cpu_sample > 0:
+        if world == 1 and not use_dist and args.cpu_sample > 0:
             try:
                 line["cpu_baseline"] = cpu_baseline(r, args.seed, args.cpu_sample)
             except Exception as ex:  # a missing baseline must not hide the GPU number

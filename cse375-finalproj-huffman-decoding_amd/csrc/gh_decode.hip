@@ -1659,14 +1659,28 @@ inline size_t tile_lds_bytes(size_t lut_bytes, size_t stage_bytes) {
 }
 
 // Poll a granule until it carries this launch's epoch with the wanted flag (bounded).
+// Bounded by wall time, 4 s of the 100 MHz clock: a persistent grid that shares the GPU
+// with another kernel (another stream or process) waits for its not-yet-resident
+// workgroups until that kernel's workgroups retire — a delay, not a fault.  After a
+// timeout every later poll returns at once (the decode then fails with GH_E_HIP).
+// The clock and the status word are read only every 64th poll: a poll's load sits in
+// the CU's memory queue behind its streaming traffic (microseconds), and the look-back
+// chain pays every extra round trip.
 __device__ __forceinline__ unsigned long long poll_granule(const TileParams& p,
                                                            unsigned long long* g, uint32_t flag) {
-  for (uint32_t spins = 0;; ++spins) {
+  unsigned long long t0 = 0;
+  for (uint32_t spins = 1;; ++spins) {
     const unsigned long long v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if ((uint32_t)(v >> 40) == p.epoch && (uint32_t)((v >> 38) & 3u) == flag) return v;
-    if (spins > SPIN_LIMIT) {
-      atomicOr(p.status, (unsigned)GH_ST_TIMEOUT);
-      return 0;
+    if ((spins & 63u) == 0u) {
+      if (__hip_atomic_load(p.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & GH_ST_TIMEOUT) return 0;
+      const unsigned long long t = wall_clock64();
+      if (t0 == 0) {
+        t0 = t;
+      } else if (t - t0 > 400000000ull) {
+        atomicOr(p.status, (unsigned)GH_ST_TIMEOUT);
+        return 0;
+      }
     }
     __builtin_amdgcn_s_sleep(2);
   }
@@ -2040,7 +2054,6 @@ void gh_tile_kernel(const TileParams p) {
 
 #include "gh_msplit.hip"
 #include "gh_wsplit.hip"
-#include "gh_wtile.hip"
 
 // ============================================================================
 // Host side
@@ -2251,7 +2264,10 @@ static SplitKernels split_for(bool single, bool fb, int uv, int g) {
 #ifndef GH_TB_GRP
 #define GH_TB_GRP 512  // grouped tile path workgroup size (256: 4 per CU, measured 1.5x slower: more stragglers per round)
 #endif
-constexpr int TB_GRP = GH_TB_GRP, U_GRP = 2, TB_MUL = 1024, U_MUL = 1;
+#ifndef GH_U_GRP
+#define GH_U_GRP 2  // grouped tile path: segments per lane
+#endif
+constexpr int TB_GRP = GH_TB_GRP, U_GRP = GH_U_GRP, TB_MUL = 1024, U_MUL = 1;
 static const void* tile_kernel_for(int path, uint32_t g) {
   if (path == TP_MULTI) return (const void*)gh_tile_kernel<TB_MUL, U_MUL, TP_MULTI, 0>;
   if (path == TP_MULTI_FB) return (const void*)gh_tile_kernel<TB_MUL, U_MUL, TP_MULTI_FB, 0>;
@@ -2270,8 +2286,6 @@ struct gh_ctx {
   bool split = true;       // split mode (count / scan / write) vs the fused persistent kernel
   bool ms = false;         // lean multi-symbol split kernels (gh_msplit.hip)
   bool ws = false;         // wave-independent split kernels (gh_wsplit.hip)
-  bool wt = false;         // wave-tile kernel (gh_wtile.hip)
-  uint32_t wt_ntw = 0;     // its wave tiles holding segments
   uint32_t ws_nblocks = 0, ws_nranges = 0, ws_grid_c = 0;
   int ws_ns = 4;
   uint32_t ws_kc = 0;              // width of the wave-split count LUT
@@ -2350,7 +2364,6 @@ static void free_shard(gh_ctx* c) {
   c->d_rng_tot = nullptr;
   c->d_rng_off = nullptr;
   c->ws = false;
-  c->wt = false;
   c->d_ms_lut_c = nullptr;
   c->d_ms_lut_w = nullptr;
   c->ms = false;
@@ -2652,86 +2665,6 @@ static int ws_setup(gh_ctx* c, double avg_seg_bytes) {
   return GH_OK;
 }
 
-template <int GRP, int NS, int LPW>
-static const void* wt_kernel_gc(uint32_t kc) {
-  const int gc = ms_group(kc);
-  return gc >= 4 ? (const void*)gh_wtile_kernel<WT_NW, GRP, 4, NS, LPW>
-       : gc == 3 ? (const void*)gh_wtile_kernel<WT_NW, GRP, 3, NS, LPW>
-                 : (const void*)gh_wtile_kernel<WT_NW, GRP, 2, NS, LPW>;
-}
-template <int NS, int LPW>
-static const void* wt_kernel_lpw(uint32_t g, uint32_t kc) {
-  return g >= 4 ? wt_kernel_gc<4, NS, LPW>(kc) : g == 3 ? wt_kernel_gc<3, NS, LPW>(kc) : wt_kernel_gc<2, NS, LPW>(kc);
-}
-// g: decode codewords per window shift; kc: count-LUT width; ns: copy-out stores per lane
-// (4, or 5 for 4-bit codes: 64 U maxsyms + 32 <= 16 * 64 * ns); lpw: window loads per lane
-static const void* wt_kernel_for(uint32_t g, uint32_t kc, int ns, int lpw) {
-  if (ns >= 5) return lpw >= 2 ? wt_kernel_lpw<5, 2>(g, kc) : wt_kernel_lpw<5, 1>(g, kc);
-  return lpw >= 2 ? wt_kernel_lpw<4, 2>(g, kc) : wt_kernel_lpw<4, 1>(g, kc);
-}
-static int wt_ns(uint32_t maxsyms) { return 64u * WT_U * maxsyms + 32 <= 16u * 64 * 4 ? 4 : 5; }
-static int wt_lpw(uint32_t grid) { return grid - 1 > (uint32_t)WT_TB ? 2 : 1; }
-
-// Wave-tile kernel (gh_wtile.hip) for grouped single-symbol codes: complete, every
-// codeword within K <= 12 bits and >= 4 bits (<= 32 symbols per segment).
-static int wt_setup(gh_ctx* c) {
-  const uint32_t K = c->tables.K;
-  c->tile_g = std::min<uint32_t>(4, 32 / std::max<uint32_t>(c->canon.maxlen, 1));
-  std::vector<uint32_t> lt(1u << K);
-  for (uint32_t i = 0; i < (1u << K); ++i) lt[i] = c->tables.lut2[i].x | c->tables.lut2[i].y;
-  GH_HIP(hipMalloc(&c->d_lut_t, 4ull << K));
-  GH_HIP(hipMemcpy(c->d_lut_t, lt.data(), 4ull << K, hipMemcpyHostToDevice));
-  // count LUT (the wave split's end-mask entries), at most 12 bits (16 KiB of LDS)
-  {
-    const uint32_t kc = std::min<uint32_t>(ws_count_bits(c->canon), std::max<uint32_t>(12, c->canon.maxlen));
-    std::vector<uint32_t> lc;
-    ws_count_lut(c->canon, kc, &lc);
-    GH_HIP(hipMalloc(&c->d_ws_lut_c, 4ull << kc));
-    GH_HIP(hipMemcpy(c->d_ws_lut_c, lc.data(), 4ull << kc, hipMemcpyHostToDevice));
-    c->ws_kc = kc;
-  }
-  const size_t lutc_bytes = 4ull << c->ws_kc;
-  // one staging buffer holds a wave tile's worst case (64 U segments x maxsyms)
-  c->stage_bytes =
-      (uint32_t)((STAGE_PAD + 64ull * WT_U * c->tables.maxsyms_seg + 32 + 15) & ~15ull);
-  // decode-LUT replication 2^lgr: the largest that keeps the best occupancy
-  if (64ull * WT_U * c->tables.maxsyms_seg + 32 > 16ull * 64 * 5) return fail(GH_E_HIP, "wave tile too large");
-  const void* kern = wt_kernel_for(c->tile_g, c->ws_kc, wt_ns(c->tables.maxsyms_seg), 2);
-  const char* envr = getenv("GH_LGR");
-  const int lg = envr ? std::clamp(atoi(envr), 0, 14 - (int)K) : std::min(4, 14 - (int)K);
-  int best = 0, best_lg = 0;
-  for (int l2 = lg; l2 >= 0; --l2) {
-    int pc = 0;
-    GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &pc, kern, WT_TB, wt_lds_bytes<WT_NW>(4ull << (K + l2), lutc_bytes, c->stage_bytes)));
-    if (pc > best) {
-      best = pc;
-      best_lg = l2;
-    }
-    if (envr) break;
-  }
-  if (best < 1) return fail(GH_E_HIP, "wave-tile kernel does not fit on a CU");
-  c->lgr = (uint32_t)best_lg;
-  c->lut_bytes = 4ull << (K + best_lg);
-  c->lds = wt_lds_bytes<WT_NW>(c->lut_bytes, lutc_bytes, c->stage_bytes);
-  c->ntiles = (uint32_t)ceil_div(c->nseg, (uint64_t)64 * WT_U * WT_NW);
-  c->wt_ntw = (uint32_t)ceil_div(c->nseg, (uint64_t)64 * WT_U);
-  int per_cu = best;
-  if (const char* ep = getenv("GH_TILE_PERCU")) per_cu = std::clamp(atoi(ep), 1, per_cu);  // diagnostics
-  // each lane of a workgroup loads at most two aggregates of a window: G - 1 <= 2 * 64 * NW
-  c->grid = (uint32_t)std::min<uint64_t>({(uint64_t)c->ntiles, (uint64_t)per_cu * c->num_cu,
-                                          (uint64_t)2 * WT_TB + 1});
-  c->tb = WT_TB;
-  c->super = WT_U;
-  GH_HIP(hipMalloc(&c->d_tile_junk, 16ull * c->grid * WT_TB));
-  c->wt = true;
-  c->tile = false;
-  c->split = false;
-  c->ms = false;
-  c->ws = false;
-  return GH_OK;
-}
-
 // End bit of the stream's last segment (segment-relative) under the reference rule
 // "codewords starting before bit 128" (decoder.cu:529-569), its zero padding
 // decoded like the reference's: the end of the last codeword starting before 128.
@@ -2795,12 +2728,6 @@ extern "C" int gh_ctx_create(int device, gh_ctx** out) {
     for (uint32_t gv : {2u, 3u, 4u})
       (void)hipFuncSetAttribute(tile_kernel_for(tp, gv), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024);
-  for (uint32_t gv : {2u, 3u, 4u})
-    for (uint32_t kc : {7u, 10u, 12u})
-      for (int ns : {4, 5})
-        for (int lpw : {1, 2})
-          (void)hipFuncSetAttribute(wt_kernel_for(gv, kc, ns, lpw), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    160 * 1024);
   for (int gv : {0, 2, 3, 4})
     for (bool sg : {false, true})
       for (bool fbv : {false, true})
@@ -2902,14 +2829,8 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
     // GH_MODE=tile); split kernels otherwise (measured faster for the multi-symbol
     // paths, whose tile staging allows one workgroup per CU).  GH_MODE=fused|split
     // override.
-    const bool want_wt = c->nseg < (1ull << 31) && c->tables.g > 0 &&
-                         (envm ? !strcmp(envm, "wtile") : GH_WT_DEFAULT);
-    c->tile = c->nseg < (1ull << 31) && (envm ? !strcmp(envm, "tile") : c->tables.g > 0) && !want_wt;
-    c->split = !c->tile && !want_wt && (envm ? !strcmp(envm, "split") : c->tables.g == 0);
-    if (want_wt) {
-      rc = wt_setup(c);
-      if (rc) return rc;
-    }
+    c->tile = c->nseg < (1ull << 31) && (envm ? !strcmp(envm, "tile") : c->tables.g > 0);
+    c->split = !c->tile && (envm ? !strcmp(envm, "split") : c->tables.g == 0);
     if (c->tile) {
       const bool grouped = c->tables.g > 0;
       c->tile_path = grouped ? TP_GROUPED : c->tables.needs_fb ? TP_MULTI_FB : TP_MULTI;
@@ -3027,8 +2948,8 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
       GH_HIP(hipMalloc(&c->d_tile_cnt, 4ull * c->ntiles + 16));
       GH_HIP(hipMalloc(&c->d_wg_tot, 8ull * c->grid * c->count_per + 16));
     }
-    if (!c->tile && !c->ms && !c->ws && !c->wt) c->tb = c->split ? TB_S : c->tables.g > 0 ? TB_G : TB;
-    for (; !c->split && !c->tile && !c->ms && !c->ws && !c->wt; uv >>= 1) {  // fall back to a narrower ILP width if the kernel does not fit
+    if (!c->tile && !c->ms && !c->ws) c->tb = c->split ? TB_S : c->tables.g > 0 ? TB_G : TB;
+    for (; !c->split && !c->tile && !c->ms && !c->ws; uv >>= 1) {  // fall back to a narrower ILP width if the kernel does not fit
       c->super = (uint32_t)uv;
       c->stage_bytes = (uint32_t)(((uint64_t)uv * c->tb * c->tables.maxsyms_seg + 64 + 15) & ~15ull);
       c->lds = lut_bytes + FB_BYTES + 2 * c->stage_bytes + SCRATCH_BYTES;
@@ -3046,13 +2967,13 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
     if (c->grid == 0) return fail(GH_E_HIP, "decode kernel does not fit on a CU");
     if (c->tile) GH_HIP(hipMalloc(&c->d_tile_junk, 16ull * c->grid * c->tb));
 #ifdef GH_STAMPS
-    GH_HIP(hipMalloc(&c->d_stamps, 16ull * 8 * 8 * c->grid));  // 16 per wave (wtile), per block (others)
-    GH_HIP(hipMemset(c->d_stamps, 0, 16ull * 8 * 8 * c->grid));
+    GH_HIP(hipMalloc(&c->d_stamps, 16ull * 8 * c->grid));
+    GH_HIP(hipMemset(c->d_stamps, 0, 16ull * 8 * c->grid));
 #endif
   }
   // look-back granules; tile mode adds the within-round prefixes and the round offsets
   c->gran_words = std::max<uint64_t>(c->ntiles, 1);
-  if (c->tile || c->wt)
+  if (c->tile)
     c->gran_words = 2ull * c->ntiles + ceil_div(c->ntiles, std::max<uint32_t>(c->grid, 1)) + 2;
   GH_HIP(hipMalloc(&c->d_gran, 8ull * c->gran_words));
   GH_HIP(hipMemset(c->d_gran, 0, 8ull * c->gran_words));
@@ -3098,7 +3019,7 @@ extern "C" int gh_ctx_load(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e
                      hipMemcpyHostToDevice));
   c->gap_nib0 = (uint32_t)(b - 8 * gw0);
   c->ms_last_end = 0;
-  if ((c->ms || c->ws || c->wt) && e == s->g) {
+  if ((c->ms || c->ws) && e == s->g) {
     uint32_t w5[5] = {};
     for (uint64_t i = 0; i < 5; ++i)
       if (4 * (e - 1) + i < s->w) std::memcpy(&w5[i], (const uint8_t*)s->payload + 4 * (4 * (e - 1) + i), 4);
@@ -3144,7 +3065,7 @@ extern "C" int gh_ctx_load_device(gh_ctx* c, const gh_stream* s, uint64_t b, uin
     c->first_start = (wv >> (4 * (nib & 7))) & 15u;
   }
   c->ms_last_end = 0;
-  if ((c->ms || c->ws || c->wt) && e == s->g) {
+  if ((c->ms || c->ws) && e == s->g) {
     uint32_t w5[5] = {};
     const uint64_t lw0 = 4 * (c->nseg - 1);  // local word of the last segment
     const uint64_t nw = std::min<uint64_t>(5, have > lw0 ? have - lw0 : 0);
@@ -3193,7 +3114,7 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     c->done_rec = true;
     return GH_OK;
   }
-  if (++c->epoch >= (c->wt ? 0x10000u : EPOCH_MAX)) {  // granule epochs wrap: start clean
+  if (++c->epoch >= EPOCH_MAX) {  // granule epochs wrap: start clean
     GH_HIP(hipMemsetAsync(c->d_gran, 0, 8ull * c->gran_words, st));
     c->epoch = 1;
   }
@@ -3224,6 +3145,17 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     p.ablate = ab ? (unsigned)atoi(ab) : 0u;
     const char* sc = getenv("GH_SCHED");
     p.sched = (sc && !strcmp(sc, "dynamic")) ? 0u : 1u;
+  }
+  // Persistent kernels (tile, wave tile, fused) are chained per device: wait for the
+  // previous one before the start event, so a decode's time excludes its queueing
+  // behind other contexts' decodes.
+  const bool chained = c->tile || (!c->ws && !c->ms && !c->split);
+  DevChain& dc = dev_chain(c->device);
+  std::unique_lock<std::mutex> chain_lock(dc.mu, std::defer_lock);
+  if (chained) {
+    chain_lock.lock();
+    if (!dc.last) GH_HIP(hipEventCreateWithFlags(&dc.last, hipEventDisableTiming));
+    if (dc.has) GH_HIP(hipStreamWaitEvent(st, dc.last, 0));
   }
   std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
   if (timed) {
@@ -3311,49 +3243,7 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     const MsKernels mk = ms_kernels(c->ms_k, c->ms_wu);
     GH_HIP(hipLaunchKernel(mk.count, dim3(c->grid * c->count_per), dim3(TB_MS), ac, c->lds_count, st));
     GH_HIP(hipLaunchKernel(mk.write, dim3(c->grid), dim3(mk.tbw), aw, c->lds, st));
-  } else if (c->wt) {
-    DevChain& dc = dev_chain(c->device);
-    std::lock_guard<std::mutex> chain_lock(dc.mu);
-    if (!dc.last) GH_HIP(hipEventCreateWithFlags(&dc.last, hipEventDisableTiming));
-    if (dc.has) GH_HIP(hipStreamWaitEvent(st, dc.last, 0));
-    WtParams t{};
-    t.payload = c->d_payload;
-    t.gaps = c->d_gaps;
-    t.lut = c->d_lut_t;
-    t.out = c->d_out;
-    t.agg = (unsigned int*)c->d_gran;
-    t.lutc = c->d_ws_lut_c;
-    t.kcbits = c->ws_kc;
-    t.lutc_bytes = 4u << c->ws_kc;
-    t.last_end = c->ms_last_end;
-    t.status = c->d_misc + 1;
-    t.total = (unsigned long long*)(c->d_misc + 2);
-    t.junk = c->d_tile_junk;
-    t.out_cap = c->out_cap;
-    t.nseg = (uint32_t)c->nseg;
-    t.ntiles = c->ntiles;
-    t.ntw = c->wt_ntw;
-    t.gap_nib0 = c->gap_nib0;
-    t.first_start = c->first_start;
-    t.kbits = c->tables.K;
-    t.lgr = c->lgr;
-    t.epoch = c->epoch;
-    t.lut_bytes = (uint32_t)c->lut_bytes;
-    t.stage_bytes = c->stage_bytes;
-    t.stamps = c->d_stamps;
-    static thread_local void* ta[1];
-    static thread_local WtParams tp;
-    tp = t;
-    ta[0] = &tp;
-    GH_HIP(hipLaunchKernel(wt_kernel_for(c->tile_g, c->ws_kc, wt_ns(c->tables.maxsyms_seg), wt_lpw(c->grid)),
-                           dim3(c->grid), dim3(WT_TB), ta, c->lds, st));
-    GH_HIP(hipEventRecord(dc.last, st));
-    dc.has = true;
   } else if (c->tile) {
-    DevChain& dc = dev_chain(c->device);
-    std::lock_guard<std::mutex> chain_lock(dc.mu);
-    if (!dc.last) GH_HIP(hipEventCreateWithFlags(&dc.last, hipEventDisableTiming));
-    if (dc.has) GH_HIP(hipStreamWaitEvent(st, dc.last, 0));
     TileParams t{};
     t.payload = c->d_payload;
     t.gaps = c->d_gaps;
@@ -3397,10 +3287,6 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
                            c->lds_count, st));
     GH_HIP(hipLaunchKernel(k.write, dim3(c->grid), dim3(TB_S), args_of(p), c->lds, st));
   } else {
-    DevChain& dc = dev_chain(c->device);
-    std::lock_guard<std::mutex> chain_lock(dc.mu);
-    if (!dc.last) GH_HIP(hipEventCreateWithFlags(&dc.last, hipEventDisableTiming));
-    if (dc.has) GH_HIP(hipStreamWaitEvent(st, dc.last, 0));
     GH_HIP(hipLaunchKernel(kernel_for(c->tables.single, c->tables.needs_fb, (int)c->super,
                                       c->tables.g),
                            dim3(c->grid), dim3(c->tb), args_of(p), c->lds, st));
@@ -3450,8 +3336,7 @@ extern "C" int gh_ctx_report(gh_ctx* c, void* hip_stream, gh_report* rep) {
     rep->lut_bits = c->tables.K;
     rep->grid = c->grid;
     rep->tiles = c->ntiles;
-    rep->mode = c->wt ? GH_MODE_WTILE : c->tile ? GH_MODE_TILE
-                : (c->split || c->ms || c->ws) ? GH_MODE_SPLIT : GH_MODE_FUSED;
+    rep->mode = c->tile ? GH_MODE_TILE : (c->split || c->ms || c->ws) ? GH_MODE_SPLIT : GH_MODE_FUSED;
     std::memcpy(&rep->slow_lookbacks, misc + 4, 8);
     rep->path = c->ws ? GH_PATH_MULTI_WAVE : c->ms ? GH_PATH_MULTI_LEAN
                 : c->tables.g > 0 ? GH_PATH_GROUPED : c->tables.single ? GH_PATH_SINGLE : GH_PATH_MULTI;
@@ -3575,7 +3460,7 @@ extern "C" int gh_debug_stats(gh_ctx* c, unsigned long long* host) {
 // Diagnostic build only: per-block phase cycle totals of the last launch.
 extern "C" int gh_debug_stamps(gh_ctx* c, unsigned long long* host, uint32_t max_blocks) {
   if (!c || !host || !c->d_stamps) return fail(GH_E_ARG, "no stamps");
-  const uint32_t nb = std::min(max_blocks, c->wt ? c->grid * (uint32_t)WT_NW : c->grid);  // rows of 16
+  const uint32_t nb = std::min(max_blocks, c->grid);
   GH_HIP(hipDeviceSynchronize());
   GH_HIP(hipMemcpy(host, c->d_stamps, 16ull * 8 * nb, hipMemcpyDeviceToHost));
   return (int)nb;

@@ -47,6 +47,26 @@ constexpr int WS_SCAN_TB = 1024;
 #ifndef GH_WS_BF
 #define GH_WS_BF 1  // branch-free staging: every lane ORs (zero past its end), one 64-bit shift per lookup
 #endif
+#ifndef GH_WS_PRIO
+#define GH_WS_PRIO 4  // rotate s_setprio over 4 workgroup slots by block (0: off); cfg3 0.579 -> 0.565 ms
+#endif
+// Workgroups dispatched later to a CU lose issue-arbitration ties to earlier ones (age
+// order), so with static ranges the later slots finish last; rotating the priority by
+// block gives every slot the lead in turn.  Slot = blockIdx / (grid / slots).
+#if GH_WS_PRIO
+#define WS_PRIO(blk, b, g)                                                            \
+  do {                                                                                \
+    const uint32_t slot_ = (b) / max(1u, (g) / (uint32_t)GH_WS_PRIO);                 \
+    switch (((blk) + slot_) % (uint32_t)GH_WS_PRIO) {                                 \
+      case 0: __builtin_amdgcn_s_setprio(0); break;                                   \
+      case 1: __builtin_amdgcn_s_setprio(1); break;                                   \
+      case 2: __builtin_amdgcn_s_setprio(2); break;                                   \
+      default: __builtin_amdgcn_s_setprio(3); break;                                  \
+    }                                                                                 \
+  } while (0)
+#else
+#define WS_PRIO(blk, b, g) do {} while (0)
+#endif
 #ifndef GH_WS_ABLATE
 #define GH_WS_ABLATE 0  // diagnostic builds only (results wrong): 1 no LDS OR, 2 no stores, 4 no copy-out
 #endif
@@ -152,6 +172,7 @@ __global__ __launch_bounds__(TBK) void gh_ws_count_kernel(const WsParams p) {
     uint32_t tot = 0;
     if (b0 < b1) ws_load<U>(p, b0, lane, w, w4, ga, gb);
     for (uint32_t blk = b0; blk < b1; ++blk) {
+      WS_PRIO(blk, blockIdx.x, gridDim.x);
       Win v[U];
       int R[U];
       uint32_t cnt[U];
@@ -311,6 +332,7 @@ __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
   uint4* junk = p.junk + ((unsigned long long)(blockIdx.x * (uint32_t)NWAVE + (uint32_t)wid) * 64u + lane);
   bool capped = false;  // the output ended at out_cap inside an earlier piece: nothing more to write
   for (uint32_t blk = b0; blk < b1 && !capped; ++blk) {
+    WS_PRIO(blk, blockIdx.x, gridDim.x);
     {
       int start[U];
       uint32_t cc[U];

@@ -105,7 +105,7 @@ class gh_sync_report(ctypes.Structure):
                 ("kernel_ms", ctypes.c_float)]
 
 
-MODE_NAMES = {0: "fused", 1: "split", 2: "tile", 3: "wtile"}
+MODE_NAMES = {0: "fused", 1: "split", 2: "tile"}
 PATH_NAMES = {0: "multi", 1: "single", 2: "grouped", 3: "multi_lean", 4: "multi_wave"}
 
 

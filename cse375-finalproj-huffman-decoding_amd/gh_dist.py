@@ -77,6 +77,30 @@ def share_stream(dist, rank: int, path: str, make_image: Callable[[], np.ndarray
     return {"n": n, "w": w, "g": g, "version": ver, "file_bytes": fb}
 
 
+def pick_share_dir(dist, rank: int, want_bytes: int, preferred: str, device,
+                   fallbacks: Optional[List[str]] = None) -> str:
+    """Directory for the shared stream file: `preferred` (normally /dev/shm, RAM-backed)
+    when it has room for `want_bytes` plus 64 MiB, else the first fallback that does
+    (TMPDIR, /tmp, the working directory).  Rank 0 decides (every rank of one node
+    sees the same filesystems) and broadcasts its choice; raises when none fits."""
+    cands = [preferred] + [d for d in (fallbacks if fallbacks is not None else
+                                       [os.environ.get("TMPDIR", ""), "/tmp", os.getcwd()]) if d]
+    pick = [-1]
+    if rank == 0:
+        for i, d in enumerate(cands):
+            try:
+                st = os.statvfs(d)
+            except OSError:
+                continue
+            if os.access(d, os.W_OK) and st.f_bavail * st.f_frsize >= want_bytes + (64 << 20):
+                pick = [i]
+                break
+    (i,) = _bcast_ints(dist, pick, device)
+    if i < 0:
+        raise RuntimeError(f"no directory with {want_bytes} free bytes for the shared stream: {cands}")
+    return cands[i]
+
+
 def exclusive_offsets(dist, count: int, device) -> Tuple[int, List[int]]:
     """Output byte offset of this rank's shard (exclusive scan of shard sizes) and
     the list of all shard sizes, via one all_gather of one integer per rank."""

@@ -148,7 +148,7 @@ typedef struct gh_report {
   uint32_t tiles;          /* segment tiles in the shard                            */
   float kernel_ms;         /* average time of one decode (all its kernels), events  */
   uint32_t launches;       /* decodes averaged in kernel_ms                         */
-  uint32_t mode;           /* GH_MODE_FUSED, _SPLIT, _TILE or _WTILE                 */
+  uint32_t mode;           /* GH_MODE_FUSED, GH_MODE_SPLIT or GH_MODE_TILE          */
   uint32_t path;           /* GH_PATH_*: table / decode-loop variant                */
   uint64_t slow_lookbacks; /* tile mode: look-backs that needed the slow path        */
 } gh_report;
@@ -156,7 +156,6 @@ typedef struct gh_report {
 #define GH_MODE_FUSED 0u    /* one persistent kernel, decoupled look-back            */
 #define GH_MODE_SPLIT 1u    /* count kernel + write kernel                           */
 #define GH_MODE_TILE 2u     /* persistent tile kernel, look-back per tile            */
-#define GH_MODE_WTILE 3u    /* persistent wave-tile kernel, no workgroup barrier     */
 #define GH_PATH_MULTI 0u    /* multi-symbol LUT, count + emit passes                 */
 #define GH_PATH_SINGLE 1u   /* single-symbol LUT, one pass (fallback for long codes) */
 #define GH_PATH_GROUPED 2u  /* single-symbol LUT, grouped window shifts              */

@@ -100,3 +100,48 @@ def test_shard_alg_bytes():
     assert gh_dist.shard_alg_bytes(w=40, begin=0, end=10, out_bytes=100) == 4 * 40 + 4 * 2 + 100
     # interior shard reads one word past its last segment (spanning codeword)
     assert gh_dist.shard_alg_bytes(w=400, begin=8, end=16, out_bytes=7) == 4 * 33 + 4 * 1 + 7
+
+
+def _pick_worker(rank, world, port, dirs, want, q):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "cse375-finalproj-huffman-decoding_amd"))
+    import torch.distributed as dist
+
+    import gh_dist
+
+    try:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                                world_size=world)
+        try:
+            got = gh_dist.pick_share_dir(dist, rank, want, dirs[0], "cpu", fallbacks=dirs[1:])
+        except RuntimeError:
+            got = None
+        q.put((rank, got, None))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as ex:  # pragma: no cover - reported to the parent
+        q.put((rank, None, repr(ex)))
+
+
+@pytest.mark.parametrize("case", ["fits", "fallback", "none"])
+def test_share_dir_free_space_gloo(case, tmp_path):
+    """bench.py's shared stream file: rank 0 checks the preferred directory's free space
+    (os.statvfs) and falls back to the next directory that has room; every rank gets the
+    same answer (a broadcast), and no room anywhere is an error on every rank."""
+    free = os.statvfs(str(tmp_path)).f_bavail * os.statvfs(str(tmp_path)).f_frsize
+    missing = str(tmp_path / "does_not_exist")
+    dirs = {"fits": [str(tmp_path), missing], "fallback": [missing, str(tmp_path)],
+            "none": [missing, missing]}[case]
+    want = 1 << 20 if case != "none" else free * 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pick_worker, args=(k, 2, port, dirs, want, q)) for k in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    assert all(x[2] is None for x in res), res
+    expect = None if case == "none" else str(tmp_path)
+    assert [x[1] for x in res] == [expect, expect]
