@@ -118,6 +118,7 @@ def cpu_baseline(r: float, seed: int, sample: int) -> dict:
         base = {"value": round(sample / dt / 1e9, 6), "unit": "GB/s", "cores": 1, "kind": "port",
                 "sample": f"{sample} B generate(r={r}, seed={seed}); oracle bit-serial decode, "
                           f"{dt:.3f} s, verified {bool(np.array_equal(dec, data))}"}
+    if oracle.ref_available("sequential"):
         # BASELINE configs[0] literally: sequential.cpp on 10 MB of redundancy-0.5 data
         try:
             d1 = gh.generate(seed, 0.5, 10**7)
