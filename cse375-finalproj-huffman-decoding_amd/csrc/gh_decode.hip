@@ -2289,6 +2289,7 @@ struct gh_ctx {
   uint32_t ws_nblocks = 0, ws_nranges = 0, ws_grid_c = 0;
   int ws_ns = 4;
   uint32_t ws_kc = 0;              // width of the wave-split count LUT
+  bool ws_fb = false;              // wave split with the canonical fallback (long / incomplete codes)
   uint32_t* d_ws_lut_c = nullptr;  // its u32 entries {b | end mask << 16}
   uint4* d_ws_junk = nullptr;
   uint4* d_tile_junk = nullptr;  // tile mode: one 16-byte slot per thread of the grid
@@ -2412,7 +2413,7 @@ static MsKernels ms_kernels(uint32_t K, int wu) {
 // the K bits i: count LUT {b = their bits, end mask (bit e-1 per codeword end e)},
 // write LUT {their symbols (byte k = k-th), b | n << 8}.  Requires a complete code
 // with maxlen <= K, so every entry holds at least one codeword.
-static int ms_build_luts(gh_ctx* c, uint32_t K) {
+static int ms_build_luts(gh_ctx* c, uint32_t K, bool allow_fb = false) {
   const Canon& cn = c->canon;
   std::vector<uint2> lc(1u << K), lw(1u << K);
   for (uint32_t i = 0; i < (1u << K); ++i) {
@@ -2427,7 +2428,7 @@ static int ms_build_luts(gh_ctx* c, uint32_t K) {
       pos += l;
       mask |= 1u << (pos - 1);
     }
-    if (n == 0) return fail(GH_E_TABLE, "msplit: LUT entry without a codeword");
+    if (n == 0 && !allow_fb) return fail(GH_E_TABLE, "msplit: LUT entry without a codeword");
     lc[i] = make_uint2(pos, mask);
     lw[i] = make_uint2(syms, pos | (n << 8));
   }
@@ -2443,7 +2444,7 @@ static int ms_build_luts(gh_ctx* c, uint32_t K) {
 // LUT width of the multi-symbol split kernels: GH_MS_K, default 10, at least maxlen.
 static uint32_t ms_lut_bits(const Canon& cn) {
   const char* ek = getenv("GH_MS_K");
-  return (uint32_t)std::clamp(ek ? atoi(ek) : 10, (int)std::max<uint32_t>(cn.maxlen, 2), 12);
+  return (uint32_t)std::clamp(ek ? atoi(ek) : 10, (int)std::min<uint32_t>(std::max<uint32_t>(cn.maxlen, 2), 12), 12);
 }
 static int ms_setup(gh_ctx* c) {
   const Canon& cn = c->canon;
@@ -2500,17 +2501,19 @@ struct WsKernels {
   const void* count;
   const void* write;
 };
-template <int GL>
+template <int GL, bool FB = false>
 static const void* ws_write_ns(int ns) {
-  return ns <= 2 ? (const void*)gh_ws_write_kernel<WS_U, WS_TB, GL, 2>
-         : ns <= 3 ? (const void*)gh_ws_write_kernel<WS_U, WS_TB, GL, 3>
-         : ns <= 4 ? (const void*)gh_ws_write_kernel<WS_U, WS_TB, GL, 4>
-         : ns <= 6 ? (const void*)gh_ws_write_kernel<WS_U, WS_TB, GL, 6>
-                   : (const void*)gh_ws_write_kernel<WS_U, WS_TB, GL, 8>;
+  return ns <= 2 ? (const void*)gh_ws_write_kernel<WS_U, WS_TB, GL, 2, FB>
+         : ns <= 3 ? (const void*)gh_ws_write_kernel<WS_U, WS_TB, GL, 3, FB>
+         : ns <= 4 ? (const void*)gh_ws_write_kernel<WS_U, WS_TB, GL, 4, FB>
+         : ns <= 6 ? (const void*)gh_ws_write_kernel<WS_U, WS_TB, GL, 6, FB>
+                   : (const void*)gh_ws_write_kernel<WS_U, WS_TB, GL, 8, FB>;
 }
 // Count kernel by its LUT width Kc, write kernel by K and NS (store instructions per
-// lane per piece: the typical piece's 16-byte chunks / 64).
-static WsKernels ws_kernels(uint32_t Kc, uint32_t K, int ns) {
+// lane per piece: the typical piece's 16-byte chunks / 64).  fb: codes longer than the
+// tables or incomplete codes (canonical fallback, two lookups per window shift).
+static WsKernels ws_kernels(uint32_t Kc, uint32_t K, int ns, bool fb = false) {
+  if (fb) return {(const void*)gh_ws_count_kernel<WS_UC, WS_TBC, 2, true>, ws_write_ns<2, true>(ns)};
   const int gc = ms_group(Kc), g = ms_group(K);
   const void* cnt = gc >= 4 ? (const void*)gh_ws_count_kernel<WS_UC, WS_TBC, 4>
                     : gc == 3 ? (const void*)gh_ws_count_kernel<WS_UC, WS_TBC, 3>
@@ -2545,7 +2548,7 @@ static double ws_count_lut(const Canon& cn, uint32_t Kc, std::vector<uint32_t>* 
 // of ~7 ops each plus ~11 ops of window shift and mask upkeep per chain.  GH_WS_KC
 // overrides (tests).
 static uint32_t ws_count_bits(const Canon& cn) {
-  const uint32_t lo = std::max<uint32_t>(cn.maxlen, 2);
+  const uint32_t lo = std::min<uint32_t>(std::max<uint32_t>(cn.maxlen, 2), 13);  // longer codes: fallback
   if (const char* e = getenv("GH_WS_KC")) return (uint32_t)std::clamp(atoi(e), (int)lo, 14);
   uint32_t best = lo;
   double best_eff = -1;
@@ -2571,7 +2574,7 @@ static int ws_ns_for(double avg_seg_bytes) {
 // table must win by 5 % (its LDS costs occupancy).  GH_MS_K overrides.
 static uint32_t ws_write_bits(const Canon& cn) {
   if (getenv("GH_MS_K")) return ms_lut_bits(cn);
-  const uint32_t lo = std::max<uint32_t>(cn.maxlen, 10);
+  const uint32_t lo = std::min<uint32_t>(std::max<uint32_t>(cn.maxlen, 10), 12);  // longer codes: fallback
   uint32_t best = lo;
   double best_eff = -1;
   for (uint32_t K = lo; K <= 12; ++K) {
@@ -2601,8 +2604,14 @@ static uint32_t ws_write_bits(const Canon& cn) {
 static int ws_setup(gh_ctx* c, double avg_seg_bytes) {
   const Canon& cn = c->canon;
   const uint32_t K = ws_write_bits(cn);
-  if (int rc = ms_build_luts(c, K)) return rc;
-  const size_t lb = c->lut_bytes;
+  // canonical fallback: codewords longer than a table, or patterns outside an incomplete
+  // code (a LUT entry with no codeword)
+  uint64_t kraft = 0;
+  for (uint32_t l = 1; l <= 16; ++l) kraft += (uint64_t)cn.count[l] << (16 - l);
+  const bool fb = kraft != 65536 || cn.maxlen > std::min<uint32_t>(K, ws_count_bits(cn));
+  c->ws_fb = fb;
+  if (int rc = ms_build_luts(c, K, fb)) return rc;
+  const size_t lb = c->lut_bytes + (fb ? (size_t)FB_BYTES : 0);  // write kernel: LUT + fallback tables
   constexpr int NW = WS_TB / 64;
   {
     const uint32_t kc = ws_count_bits(cn);
@@ -2633,10 +2642,10 @@ static int ws_setup(gh_ctx* c, double avg_seg_bytes) {
     stage = std::max<size_t>((size_t)atoll(es), (chain_worst + 15) & ~15ull) & ~15ull;
   c->stage_bytes = (uint32_t)stage;
   c->lds = lb + NW * stage;
-  c->lds_count = std::max<size_t>(4ull << c->ws_kc, 64);
+  c->lds_count = std::max<size_t>(4ull << c->ws_kc, 64) + (fb ? FB_BYTES : 0);
   c->ws_ns = ws_ns_for(avg_seg_bytes);
   if (const char* en = getenv("GH_WS_NS")) c->ws_ns = std::clamp(atoi(en), 2, 8);
-  const WsKernels k = ws_kernels(c->ws_kc, K, c->ws_ns);
+  const WsKernels k = ws_kernels(c->ws_kc, K, c->ws_ns, fb);
   int pc_c = 0, pc_w = 0;
   GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc_c, k.count, WS_TBC, c->lds_count));
   GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc_w, k.write, WS_TB, c->lds));
@@ -2905,12 +2914,9 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
     // Lean multi-symbol split kernels: multi-symbol codes that are complete and fit
     // 12 bits (GH_MODE=split / fused / tile keep the older kernels).
     {
-      uint64_t kraft = 0;
-      for (uint32_t l = 1; l <= 16; ++l) kraft += (uint64_t)c->canon.count[l] << (16 - l);
-      const bool eligible = kraft == 65536 && c->canon.maxlen <= 12 && c->canon.minlen >= 2 &&
-                            c->nseg < (1ull << 31);
+      const bool eligible = c->nseg < (1ull << 31);  // any code: long and incomplete ones use the fallback
       const bool force_ms = envm && !strcmp(envm, "msplit"), force_ws = envm && !strcmp(envm, "wsplit");
-      const bool want = envm ? (force_ms || force_ws) : (!c->tables.single && c->tables.g == 0);
+      const bool want = envm ? (force_ms || force_ws) : c->tables.g == 0;
       if (eligible && want) {
         // default: the wave-independent kernels (measured faster than msplit on cfg2/3/5)
         rc = force_ms ? ms_setup(c) : ws_setup(c, s->g ? (double)s->n / (double)s->g : 16.0);
@@ -3196,6 +3202,9 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     m.lut_bytes = (uint32_t)c->lut_bytes;
     m.stage_bytes = c->stage_bytes;
     m.last_end = c->ms_last_end;
+    m.fb = c->d_fb;
+    m.fb_lo = std::max<uint32_t>(c->canon.minlen, 1);
+    m.fb_hi = std::max<uint32_t>(c->canon.maxlen, m.fb_lo);
     static thread_local WsParams wc, ww;
     static thread_local void* ac[1];
     static thread_local void* aw[1];
@@ -3207,7 +3216,7 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     ww.lut = c->d_ms_lut_w;
     ac[0] = &wc;
     aw[0] = &ww;
-    const WsKernels wk = ws_kernels(c->ws_kc, c->ms_k, c->ws_ns);
+    const WsKernels wk = ws_kernels(c->ws_kc, c->ms_k, c->ws_ns, c->ws_fb);
     GH_HIP(hipLaunchKernel(wk.count, dim3(c->ws_grid_c), dim3(WS_TBC), ac, c->lds_count, st));
     GH_HIP(hipLaunchKernel((const void*)gh_ws_scan_kernel, dim3(1), dim3(WS_SCAN_TB), ac, 0, st));
     GH_HIP(hipLaunchKernel(wk.write, dim3(c->grid), dim3(WS_TB), aw, c->lds, st));

@@ -85,6 +85,8 @@ struct WsParams {
   unsigned long long out_cap;
   uint32_t nseg, nsb, nranges, gap_nib0, first_start, kbits, lut_bytes, stage_bytes;
   uint32_t last_end;               // != 0: end of the stream's last segment (= local segment nseg-1)
+  const uint32_t* fb;              // FB kernels: canonical tables (FB_WORDS: limit16, base16, first, symbols)
+  uint32_t fb_lo, fb_hi;           // their length range (minlen, maxlen)
   unsigned long long chk_pay, chk_gap, chk_out;  // GH_WS_CHECK builds: allocation sizes (words, words, bytes)
 };
 #ifndef GH_WS_CHECK
@@ -134,6 +136,32 @@ __device__ __forceinline__ void ws_lut_to_lds(const WsParams& p, uint8_t* smem, 
   for (uint32_t i = tid; i < p.lut_bytes / 16; i += TBK) s4[i] = g[i];
 }
 
+// Canonical decode of the codeword at the top of w16 (16 window bits) from the LDS
+// tables (gh_core's Canon: limit16 / base16 / first / symbols): (symbol << 8) | length.
+// Used where a LUT entry holds no codeword (the first one is longer than the table
+// width, or the pattern is outside an incomplete code: then `bad`, and the longest
+// length, which keeps the count and the write in step).
+// allowed-ends mask for R bits left: bit e-1 set for ends e <= R, all ones if R >= 32,
+// none once the segment is finished (R <= 0; 1-bit codewords end at offset 1).
+__device__ __forceinline__ uint32_t ws_rmask(int R) {
+  const uint32_t m = 0xFFFFFFFFu >> (32u - (uint32_t)min(max(R, 1), 32));
+  return R > 0 ? m : 0u;
+}
+
+__device__ __forceinline__ uint32_t ws_canon(const uint32_t* s_fb, uint32_t w16, uint32_t lo, uint32_t hi,
+                                             uint32_t& bad) {
+  const uint8_t* syms = (const uint8_t*)(s_fb + 51);
+  for (uint32_t l = lo; l <= hi; ++l) {
+    if (w16 < s_fb[l]) return ((uint32_t)syms[(s_fb[34 + l] + ((w16 - s_fb[17 + l]) >> (16 - l))) & 255u] << 8) | l;
+  }
+  bad = 1;
+  return ((uint32_t)syms[0] << 8) | hi;
+}
+template <int TBK>
+__device__ __forceinline__ void ws_fb_to_lds(const WsParams& p, uint32_t* s_fb, int tid) {
+  for (uint32_t i = tid; i < (uint32_t)FB_WORDS; i += TBK) s_fb[i] = p.fb[i];
+}
+
 // Count-LUT lookup results: ds_read_b32 each, one wait for the U of a step.
 template <int U>
 __device__ __forceinline__ void ws_wait32(uint32_t (&v)[U]) {
@@ -153,13 +181,20 @@ __device__ __forceinline__ void ws_wait32(uint32_t (&v)[U]) {
 //   cnt += popcount(endmask & rm)   (SDWA AND of the high half, v_bcnt)
 //   rm >>= b                        (v_ashrrev reads only the low 5 bits of the entry)
 //   q -= entry                      (q's low 16 bits stay exact: sum of b <= 32)
-template <int U, int TBK, int GL>
+// FB: codes longer than Kc or incomplete codes; an entry with no codeword (b = 0) is
+// replaced by the canonical codeword's {len, end mask 1 << (len-1)} (GL = 2 then: two
+// lookups of up to 16 bits fit one 32-bit window shift).
+template <int U, int TBK, int GL, bool FB = false>
 __global__ __launch_bounds__(TBK) void gh_ws_count_kernel(const WsParams p) {
+  static_assert(!FB || GL <= 2, "fallback lookups take up to 16 bits: two per window shift");
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t sh = 30u - p.kbits;  // index bits -> byte offset of a u32 entry
   const uint32_t amask = ((1u << p.kbits) - 1u) << 2;
+  uint32_t* s_fb = (uint32_t*)(smem + p.lut_bytes);
+  uint32_t bad = 0;
   ws_lut_to_lds<TBK>(p, smem, tid);
+  if constexpr (FB) ws_fb_to_lds<TBK>(p, s_fb, tid);
   if (tid == 0 && (uint32_t)(size_t)(const __attribute__((address_space(3))) uint8_t*)smem != 0u)
     atomicOr(p.status, (unsigned)GH_ST_LAYOUT);
   __syncthreads();
@@ -193,20 +228,27 @@ __global__ __launch_bounds__(TBK) void gh_ws_count_kernel(const WsParams p) {
         uint32_t rm[U], q[U];
   #pragma unroll
         for (int u = 0; u < U; ++u) {
-          rm[u] = ms_rmask(R[u]);
+          rm[u] = ws_rmask(R[u]);
           q[u] = 32u;
         }
   #pragma unroll
         for (int j = 0; j < GL; ++j) {
-          uint32_t e[U];
+          uint32_t e[U], xs[U];
   #pragma unroll
           for (int u = 0; u < U; ++u) {
             const uint32_t x = j == 0 ? v[u].d0 : __builtin_amdgcn_alignbit(v[u].d0, v[u].d1, q[u]);
+            xs[u] = x;
             asm volatile("ds_read_b32 %0, %1" : "=v"(e[u]) : "v"((x >> sh) & amask) : "memory");
           }
           ws_wait32(e);
   #pragma unroll
           for (int u = 0; u < U; ++u) {
+            if constexpr (FB) {
+              if ((e[u] & 0xFFFFu) == 0u) {
+                const uint32_t l = ws_canon(s_fb, xs[u] >> 16, p.fb_lo, p.fb_hi, bad) & 31u;
+                e[u] = l | ((1u << (l - 1u)) << 16);
+              }
+            }
             uint32_t m;
             asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD"
                 : "=v"(m) : "v"(e[u]), "v"(rm[u]));
@@ -234,6 +276,7 @@ __global__ __launch_bounds__(TBK) void gh_ws_count_kernel(const WsParams p) {
     unsigned long long t64 = wave_sum_u64(tot);
     if (lane == 0 && WS_CK(r < p.nranges, 0x800)) p.rng_tot[r] = t64;
   }
+  if (FB && __any(bad != 0) && lane == 0) atomicOr(p.status, (unsigned)GH_ST_BADCODE);
 }
 
 // Exclusive scan of the range totals (one workgroup), and the stream total.
@@ -288,14 +331,20 @@ __device__ __forceinline__ void ws_store_bytes(uint8_t* dst, const uint4* chunk,
 // wait for the prefetched loads with vmcnt(NS + ...) instead of vmcnt(0): on gfx950
 // loads and stores share one in-order counter, and a vmcnt(0) at the top of every block
 // made each wave wait for its previous block's stores to be acknowledged).
-template <int U, int TBK, int GL, int NS>
+// FB: an entry with no codeword (n = 0) is replaced by the canonical codeword's
+// {symbol, len | 1 << 8} (tables after the staging; GL = 2 then).
+template <int U, int TBK, int GL, int NS, bool FB = false>
 __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
+  static_assert(!FB || GL <= 2, "fallback lookups take up to 16 bits: two per window shift");
   constexpr int NWAVE = TBK / 64;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const uint32_t sh = 29u - p.kbits;
   const uint32_t amask = ((1u << p.kbits) - 1u) << 3;
+  uint32_t* s_fb = (uint32_t*)(smem + p.lut_bytes + (uint32_t)NWAVE * p.stage_bytes);
+  uint32_t bad = 0;
   ws_lut_to_lds<TBK>(p, smem, tid);
+  if constexpr (FB) ws_fb_to_lds<TBK>(p, s_fb, tid);
   for (uint32_t i = tid; i < (uint32_t)NWAVE * p.stage_bytes / 16; i += TBK)
     ((uint4*)(smem + p.lut_bytes))[i] = make_uint4(0, 0, 0, 0);
   if (tid == 0 && (uint32_t)(size_t)(const __attribute__((address_space(3))) uint8_t*)smem != 0u)
@@ -388,14 +437,22 @@ __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
 #pragma unroll
           for (int j = 0; j < GL; ++j) {
             uint2 e[U];
+            uint32_t xs[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
               const uint32_t x = j == 0 ? v[u].d0 : __builtin_amdgcn_alignbit(v[u].d0, v[u].d1, q[u]);
+              xs[u] = x;
               e[u] = ms_lds_u64((x >> sh) & amask);
             }
             ms_wait(e);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
+              if constexpr (FB) {
+                if ((e[u].y & 0x700u) == 0u) {  // n = 0
+                  const uint32_t r = ws_canon(s_fb, xs[u] >> 16, p.fb_lo, p.fb_hi, bad);
+                  e[u] = make_uint2(r >> 8, (r & 31u) | (1u << 8));
+                }
+              }
               if constexpr (GH_WS_BF) {
                 // a lane past its end ORs zero at its end (inside the staging spill)
                 const bool on = ptr[u] < end[u];
@@ -476,4 +533,5 @@ __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
     if (te != 0 && ge > rs && !(GH_WS_ABLATE & 2) && WS_CK(ge <= p.chk_out || !GH_WS_CHECK, 0x8000))
       ws_store_bytes(p.out + (ge - te), st4 + 1, hs, te, lane);
   }
+  if (FB && __any(bad != 0) && lane == 0) atomicOr(p.status, (unsigned)GH_ST_BADCODE);
 }

@@ -2,13 +2,18 @@
 # wave split do not take (codes > 12 bits or minlen 1): streams whose code lengths reach
 # 16 bits, 10^8 and 10^9 bytes.  Prints one line per stream: path, kernel time, the
 # fraction of the 8 TB/s HBM peak on algorithmic bytes, bit-exactness.
-# Usage: python scripts/time_longcodes.py
-import os, sys
+# Usage: python scripts/time_longcodes.py [--n 100000000,1000000000] [--q 0.5,0.7]
+import argparse, os, sys
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "cse375-finalproj-huffman-decoding_amd"))
 import numpy as np, gaphuff as gh
+ap = argparse.ArgumentParser()
+ap.add_argument("--n", default="100000000,1000000000")
+ap.add_argument("--q", default="0.5,0.7")
+a = ap.parse_args()
 rng = np.random.default_rng(7)
-for n in (10**8, 10**9):
-    for name, q in (("geometric_q0.5", 0.5), ("geometric_q0.7", 0.7)):
+for n in [int(x) for x in a.n.split(",")]:
+    for q in [float(x) for x in a.q.split(",")]:
+        name = f"geometric_q{q}"
         p = q ** np.arange(256, dtype=np.float64)
         p /= p.sum()
         data = rng.choice(256, size=n, p=p).astype(np.uint8)
