@@ -1,0 +1,502 @@
+// Tile kernel: the decode of grouped codes (complete, 4 <= len <= 12, e.g. BASELINE's
+// r = 0.1 data), included by gh_decode.hip.  Reference counterpart: gpu_dec_l1_l2
+// (decoder/src/decoder.cu:454-730) — its per-segment count (:529-569), decoupled
+// look-back (:571-653) and second decode that writes the bytes (:655-728) — as ONE
+// decode pass per segment in one persistent kernel.
+//
+// 512-thread workgroups, two segments per lane, a tile = 1024 consecutive segments.
+// Workgroup b takes tiles b, b + G, b + 2G, ... (static round robin over the G resident
+// workgroups; grid <= 512).  Iteration k of a workgroup:
+//
+//   decode tile k into registers (one codeword per lookup, G codewords per window shift;
+//     a codeword is kept iff it starts before the segment end: the reference's rule)
+//     - mid-decode: load the prefix of tile k-2, and, as the round leader, the round's
+//       aggregates
+//   copy tile k-2 out of staging (its prefix has had an iteration to arrive), with a
+//     fixed store count; the next tile's loads are issued just before
+//   wave scans of the counts -> BARRIER -> publish tile k's aggregate; the leader
+//     publishes its round's within-round prefixes and the next round's start
+//   stage tile k (aligned dword stores, a second barrier, the 1-3 head bytes)
+//
+// Rounds and leaders: tile rG + j is decoded in iteration r by workgroup j.  Round r's
+// leader is the workgroup that decoded tile rG + (r mod n_r); in iteration r+1 it reads
+// the round's G aggregates (one per lane, issued mid-decode), scans them and publishes
+// every tile's within-round prefix (plocal) and R[r+1] = R[r] + the round's total.  The
+// owner of a tile reads R[round] + plocal[tile] one iteration later.  Every hand-off has
+// about an iteration of slack; a decoupled look-back with 512 tiles in flight needed a
+// window of ~512 granules per tile and mostly took its slow path.
+
+constexpr int TILE_TB = 512;       // threads per workgroup
+constexpr int TILE_U = 2;          // segments per lane
+constexpr int TILE_NS = 2;         // 16-byte stores per thread per copy-out (the rest of a tile loops)
+constexpr int TILE_MIDG = 2;       // decode group after which the mid-decode loads are issued
+constexpr int STAGE_PAD = 16;      // staging byte STAGE_PAD + i = tile byte i
+constexpr int OW = 8;              // output words per segment (32 codewords of >= 4 bits)
+
+struct TileParams {
+  const uint32_t* payload;       // local segment j owns words [4j, 4j+4); +1 look-ahead, zero padded
+  const uint32_t* gaps;          // gap words; nibble (gap_nib0 + j - 1) = start of local segment j>=1
+  const uint32_t* lut;           // 2^K u32 {len | sym << 24}
+  uint8_t* out;
+  unsigned long long* granules;  // one per tile: its symbol count (flag 1)
+  unsigned long long* plocal;    // one per tile: exclusive prefix within its round (flag 2)
+  unsigned long long* rprefix;   // one per round: its starting offset (flag 2); [0] unused
+  unsigned int* status;
+  unsigned long long* total;
+  unsigned long long* stats;     // poll counters (reported as slow_lookbacks)
+  unsigned long long out_cap;
+  unsigned long long nseg;
+  unsigned int gap_nib0, first_start, ntiles, kbits, lgr, epoch;
+  unsigned int lut_bytes;        // LUT bytes in LDS (replicated: 4 << (K + lgr))
+  unsigned int stage_bytes;      // one staging buffer
+  uint4* junk;                   // 16 bytes per thread of the grid for padding stores
+};
+
+// LDS of the tile kernel: LUT, two staging buffers, wave sums, leader batch totals.
+inline size_t tile_lds_bytes(size_t lut_bytes, size_t stage_bytes) {
+  return lut_bytes + 2 * stage_bytes + 2 * (TILE_TB / 64) * 4 * TILE_U + 4 * (TILE_TB / 64) + 32;
+}
+
+// v_perm selector placing byte 3 of S0 (the symbol) at byte j, keeping S1's others.
+__device__ __forceinline__ constexpr uint32_t perm_sel(int j) {
+  return j == 0 ? 0x03020107u : j == 1 ? 0x03020700u : j == 2 ? 0x03070100u : 0x07020100u;
+}
+
+// e-window of a segment starting at bit `start` (0..15): e-stream bit 0 is segment
+// bit start - S (bits before the segment read as 0); requires 16 <= S <= 31.  The
+// lookup address of the codeword at window bit p is then
+// alignbit(e0, e1, 32 - p) & (mask << (2 + lgr)) | lane_offset: two VALU ops.
+__device__ __forceinline__ void make_ewin(uint4 w, uint32_t w4, int start, uint32_t S, uint32_t (&e)[5]) {
+  const uint32_t r = S - (uint32_t)start;  // 1..31
+  e[0] = __builtin_amdgcn_alignbit(0u, w.x, r);
+  e[1] = __builtin_amdgcn_alignbit(w.x, w.y, r);
+  e[2] = __builtin_amdgcn_alignbit(w.y, w.z, r);
+  e[3] = __builtin_amdgcn_alignbit(w.z, w.w, r);
+  e[4] = __builtin_amdgcn_alignbit(w.w, w4, r);
+}
+
+// Decode of U segments per lane on e-windows, the U chains in lock-step (their LDS
+// reads are independent, so their latencies overlap).  Each group decodes G codewords
+// per chain from e0:e1 and then shifts the windows.  q counts down from 32 by whole LUT
+// entries {len | sym << 24}: its low 24 bits stay exact, v_alignbit reads only the low
+// 5, and the liveness test q > T (the codeword starts before the segment end; T = F +
+// 32 - L, F = bits flushed so far, L = 128 - start) reads the low 16 sign-extended
+// (SDWA).  Codeword j of a segment goes to byte j of ow (v_perm, static index); dead
+// codewords go there too and are never staged.  `mid()` runs once, after group MIDG
+// (or at the end if the loop stops earlier).
+template <int G, int U, int MIDG, class Mid>
+__device__ __forceinline__ void decode_tile_grouped(uint32_t (&e)[U][5], const int (&start)[U],
+                                                    const bool (&act)[U], uint32_t (&ow)[U][OW],
+                                                    uint32_t (&cnt)[U], uint32_t amask, uint32_t laneoff,
+                                                    Mid&& mid) {
+  constexpr int S = 4 * OW;
+  constexpr int NG = (S + G - 1) / G;
+  uint32_t q[U];
+  int T[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    q[u] = 32;
+    T[u] = act[u] ? start[u] - 96 : 0x3FFFFFFF;  // inactive: never live, no overflow
+    cnt[u] = 0;
+#pragma unroll
+    for (int k = 0; k < OW; ++k) ow[u][k] = 0;
+  }
+  bool mid_done = false;
+#pragma unroll
+  for (int gi = 0; gi < NG; ++gi) {
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      const int pos = gi * G + j;
+      if (pos < S) {
+        uint32_t ent[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint32_t x = j == 0 ? e[u][0] : __builtin_amdgcn_alignbit(e[u][0], e[u][1], q[u]);
+          ent[u] = lds_u32_nowait((x & amask) | laneoff);
+        }
+        lds_wait(ent);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          asm("v_cmp_gt_i32_sdwa vcc, sext(%1), %2 src0_sel:WORD_0 src1_sel:DWORD\n\t"
+              "v_addc_co_u32 %0, vcc, 0, %0, vcc"
+              : "+v"(cnt[u]) : "v"(q[u]), "v"(T[u]) : "vcc");
+          ow[u][pos >> 2] = __builtin_amdgcn_perm(ent[u], ow[u][pos >> 2], perm_sel(pos & 3));
+          q[u] -= ent[u];
+        }
+      }
+    }
+    bool more = false;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      e[u][0] = __builtin_amdgcn_alignbit(e[u][0], e[u][1], q[u]);
+      e[u][1] = __builtin_amdgcn_alignbit(e[u][1], e[u][2], q[u]);
+      e[u][2] = __builtin_amdgcn_alignbit(e[u][2], e[u][3], q[u]);
+      e[u][3] = __builtin_amdgcn_alignbit(e[u][3], e[u][4], q[u]);
+      e[u][4] = __builtin_amdgcn_alignbit(e[u][4], 0u, q[u]);
+      T[u] += 32 - (int)(int16_t)q[u];
+      q[u] = 32;
+      more |= 32 > T[u];
+    }
+    if (gi == MIDG) {
+      mid();
+      mid_done = true;
+    }
+    if (gi + 1 < NG && !__any(more)) break;
+  }
+  if (!mid_done) mid();
+}
+
+__device__ __forceinline__ void lds_st32(uint32_t a, uint32_t v) {
+  asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+
+// Aligned staging of a segment's n bytes (ow, byte 0 first) at LDS byte address o.
+// Phase 1 writes the aligned dwords holding the segment's bytes, except the first one
+// when o is unaligned; its last dword carries whatever ow holds past byte n.  Phase 2,
+// after a workgroup barrier, writes the segment's head bytes (the 1-3 bytes of that
+// skipped first dword) exactly, over the previous segment's phase-1 tail.  Every dword
+// store is aligned: unaligned ds_write_b32 measured about 3x the LDS time of aligned
+// ones with per-lane offsets like these.  Returns the number of head bytes.
+__device__ __forceinline__ uint32_t stage_aligned_p1(const uint32_t (&ow)[OW], uint32_t n, uint32_t o) {
+  const uint32_t ap = ((o - 1u) & 3u) + 1u;  // 1..4: bytes from the dword base to o
+  const uint32_t base = o - ap;              // dword m at base + 4m holds segment bytes [4m - ap, +4)
+  const uint32_t s = 4u - ap;                // alignbyte amount
+  const uint32_t last = (n + ap - 1u) >> 2;  // last dword touched
+#pragma unroll
+  for (int m = 1; m <= OW; ++m) {
+    const uint32_t hi = m < OW ? ow[m] : 0u;
+    const uint32_t r = __builtin_amdgcn_alignbyte(hi, ow[m - 1], s);
+    if ((uint32_t)m <= last) lds_st32(base + 4u * m, r);
+  }
+  return 4u - ap;
+}
+// Phase 2: the nb (1..3) head bytes h at o (o + (nb & 1) is even).
+__device__ __forceinline__ void stage_head(uint32_t o, uint32_t h, uint32_t nb) {
+  if (nb & 1u) asm volatile("ds_write_b8 %0, %1" ::"v"(o), "v"(h) : "memory");
+  if (nb & 2u) asm volatile("ds_write_b16 %0, %1" ::"v"(o + (nb & 1u)), "v"(h >> (8u * (nb & 1u))) : "memory");
+}
+
+// Copy a tile staged at staging byte STAGE_PAD + i = tile byte i to out[goff, goff+n)
+// (n already clamped at out_cap).  Output chunk c (16 bytes, aligned to the global
+// address) is staging bytes [16c + s, +16), s = 16 - (goff & 15): one unaligned
+// ds_read_b128 (gfx950 LDS runs in unaligned mode).  A fixed number of store
+// instructions per thread: NS 16-byte stores (interior chunks; spare threads store the
+// last interior chunk again, the same bytes, merged in L2) and one byte store (a byte of
+// the two partial edge chunks, or the first edge byte again); the thread's junk slot
+// only when there is nothing to duplicate.  gfx950 counts loads and stores in one
+// in-order queue (vmcnt): with a fixed store count after the next tile's prefetch loads
+// the compiler waits for those loads with vmcnt(NS + 1) instead of vmcnt(0), so a wave
+// no longer waits for its previous copy-out's stores to be acknowledged.  Chunks beyond
+// NS per thread (a tile larger than 16 * NS * TB bytes) loop.  stg: absolute LDS byte
+// address of the staging buffer.
+template <int TBK, int NS>
+__device__ __forceinline__ void copy_out_tile(uint8_t* out, uint32_t stg, unsigned long long goff, uint32_t n,
+                                              int tid, uint4* junk) {
+  const uint32_t lb = (uint32_t)(goff & 15);
+  uint8_t* o = out + (goff - lb);          // 16-byte aligned
+  const uint32_t src = stg + 16u - lb;     // staging address of output chunk 0
+  const uint32_t cf = lb ? 1u : 0u;        // interior chunks [cf, ce)
+  const uint32_t ce = n ? (lb + n) >> 4 : 0u;
+  const bool have = ce > cf;
+#pragma unroll
+  for (int i = 0; i < NS; ++i) {
+    const uint32_t c = cf + (uint32_t)tid + (uint32_t)(TBK * i);
+    const bool real = c < ce;
+    const uint32_t cs = real ? c : ce - 1u;
+    const uint4 v = lds_u128(src + 16u * ((real || have) ? cs : cf));
+    *((real || have) ? (uint4*)(o + 16ull * cs) : junk) = v;
+  }
+  for (uint32_t c = cf + (uint32_t)tid + (uint32_t)(TBK * NS); c < ce; c += TBK)
+    *(uint4*)(o + 16ull * c) = lds_u128(src + 16u * c);
+  // edge bytes: the head chunk's [lb, min(16, lb + n)) when lb != 0, then the tail
+  // chunk's [0, (lb + n) & 15) when it is another chunk; one byte per thread
+  const uint32_t nh = (lb && n) ? min(16u, lb + n) - lb : 0u;
+  const uint32_t tl = (lb + n) & 15u;
+  const uint32_t nt = (n && tl && (ce > 0 || !lb)) ? tl : 0u;
+  const uint32_t t = (uint32_t)tid;
+  const bool hb = nh + nt > 0;
+  uint32_t k = nh ? lb : 16u * ce;  // output byte offset from o (padding: the first edge byte)
+  bool real = false;
+  if (t < nh) {
+    k = lb + t;
+    real = true;
+  } else if (t < nh + nt) {
+    k = 16u * ce + (t - nh);
+    real = true;
+  }
+  uint32_t b;
+  asm volatile("ds_read_u8 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(b) : "v"(src + ((real || hb) ? k : 0u)) : "memory");
+  *((real || hb) ? o + k : (uint8_t*)junk) = (uint8_t)b;
+}
+
+__device__ __forceinline__ bool granule_ok(const TileParams& p, unsigned long long v, uint32_t flag) {
+  return (uint32_t)(v >> 40) == p.epoch && (uint32_t)((v >> 38) & 3u) == flag;
+}
+
+// Poll a granule until it carries this launch's epoch with the wanted flag.  Bounded by
+// wall time, 4 s of the 100 MHz clock: a persistent grid that shares the GPU with
+// another kernel (another stream or process) waits for its not-yet-resident workgroups
+// until that kernel's workgroups retire — a delay, not a fault.  After a timeout every
+// later poll returns at once (the decode then fails with GH_E_HIP).  The clock and the
+// status word are read only every 64th poll: a poll's load sits in the CU's memory
+// queue behind its streaming traffic (microseconds), and the hand-off chain pays every
+// extra round trip.
+__device__ __forceinline__ unsigned long long poll_granule(const TileParams& p, unsigned long long* g,
+                                                           uint32_t flag) {
+  unsigned long long t0 = 0;
+  for (uint32_t spins = 1;; ++spins) {
+    const unsigned long long v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (granule_ok(p, v, flag)) return v;
+    if ((spins & 63u) == 0u) {
+      if (__hip_atomic_load(p.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & GH_ST_TIMEOUT) return 0;
+      const unsigned long long t = wall_clock64();
+      if (t0 == 0) {
+        t0 = t;
+      } else if (t - t0 > 400000000ull) {
+        atomicOr(p.status, (unsigned)GH_ST_TIMEOUT);
+        return 0;
+      }
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+// TB threads, U segments per lane, GRP codewords per window shift.  Compiled for at
+// most 4 waves per SIMD (two workgroups per CU: 128 VGPRs).
+template <int TB, int U, int GRP>
+__global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void gh_tile_kernel(const TileParams p) {
+  constexpr int NWAVE_T = TB / 64;
+  constexpr int LDR_NB = TB / 64;                  // leader batches: one wave per 64 * LPL tiles of a round
+  constexpr int LPL = TB >= 512 ? 1 : 1024 / TB;   // aggregates per leader lane (grid <= LPL * TB)
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* s_stage = smem + p.lut_bytes;                        // 2 buffers
+  uint32_t* s_wsum = (uint32_t*)(s_stage + 2 * p.stage_bytes);  // [2][U][NWAVE_T]
+  uint32_t* s_lead = s_wsum + 2 * U * NWAVE_T;                  // [LDR_NB]
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  {  // LUT to LDS, replicated: dword i of LDS = entry i >> lgr (lane l reads copy l mod 2^lgr,
+     // so up to 32 lanes of a ds_read_b32 hit distinct banks)
+    const uint32_t nd = p.lut_bytes >> 2;
+    uint32_t* sl = (uint32_t*)smem;
+    for (uint32_t i = tid; i < nd; i += TB) sl[i] = p.lut[i >> p.lgr];
+  }
+  const uint32_t S = 30u - p.kbits - p.lgr;
+  const uint32_t amask = ((1u << p.kbits) - 1u) << (2u + p.lgr);
+  const uint32_t laneoff = ((uint32_t)lane & ((1u << p.lgr) - 1u)) << 2;
+  check_lds_base(smem, p.status);
+  __syncthreads();
+
+  const uint32_t G = gridDim.x, b = blockIdx.x;  // grid size, workgroup
+  const uint32_t nseg = (uint32_t)p.nseg;         // < 2^31 (checked by the host)
+  constexpr uint32_t NONE = 0xFFFFFFFFu;
+  // Static round robin (a dynamic ticket order can deadlock here: a workgroup waiting
+  // for its tile's prefix may hold an undecoded tile of the same round, whose leader then
+  // waits for it).
+  const uint32_t last_tile_k = b < p.ntiles ? (p.ntiles - 1 - b) / G : NONE;
+  uint32_t cur = b, nxt = b + G;
+  uint4 w[U];
+  uint32_t w4[U], gw[U];
+  auto load = [&](uint32_t t) {
+    const uint32_t seg0 = min(t, p.ntiles - 1) * (uint32_t)(U * TB) + (uint32_t)tid;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t sc = min(seg0 + (uint32_t)(u * TB), nseg - 1);
+      w[u] = *(const uint4*)(p.payload + 4ull * sc);
+      w4[u] = p.payload[4ull * sc + 4];
+      gw[u] = p.gaps[(p.gap_nib0 + (sc ? sc - 1u : 0u)) >> 3];
+    }
+  };
+  load(cur);
+  if (cur >= p.ntiles) cur = NONE;
+  uint32_t t1 = NONE, t2 = NONE;  // tiles of iterations k-1, k-2
+  uint32_t tot1 = 0, tot2 = 0;    // their totals
+  uint32_t buf = 0;               // k & 1
+  for (uint32_t k = 0;; ++k) {
+    const bool have_cur = cur < p.ntiles;
+    const bool have2 = t2 < p.ntiles;  // tile k-2 is copied out this iteration
+    // the workgroup that decoded tile rG + (r mod n_r) leads round r (n_r tiles) one
+    // iteration later: every round, the last partial one included, has a leader
+    const uint32_t lr = t1 < p.ntiles ? t1 / G : NONE;
+    const bool lead = lr != NONE && t1 % G == lr % min(G, p.ntiles - lr * G);
+    if (!have_cur && t1 >= p.ntiles && !have2) break;
+    if (last_tile_k != NONE && k > last_tile_k + 4) {  // cannot happen; never hang the GPU
+      if (tid == 0) atomicOr(p.status, (unsigned)GH_ST_TIMEOUT);
+      break;
+    }
+    const uint32_t par = k & 1u;
+    // The second workgroup dispatched to a CU loses every issue-arbitration tie to the
+    // first (age order): alternate the two slots' priority by iteration (cfg4 0.747 ->
+    // 0.729 ms).
+    if (((k + (b >= (G >> 1) ? 1u : 0u)) & 1u) != 0u) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+    // prefix of tile k-2 (R[round] + plocal[tile], lane 0 of every wave) and the
+    // leader's R[lr] and aggregates: loaded mid-decode (a load issued at the top often saw
+    // the value a little before it was published, and the re-poll then paid a full
+    // memory round trip)
+    unsigned long long gr = 0, gp = 0, rl = 0;
+    if (lead && tid == 0 && lr > 0) rl = __hip_atomic_load(&p.rprefix[lr], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t lt = lr * G + (uint32_t)tid * LPL;  // leader: first tile of this lane
+    const uint32_t lend = min(p.ntiles, (lr + 1) * G);
+    bool lvalid[LPL];
+    unsigned long long la[LPL];
+#pragma unroll
+    for (int j = 0; j < LPL; ++j) {
+      lvalid[j] = lead && lt + j < lend;
+      la[j] = 0;
+    }
+    auto mid = [&]() {
+      if (have2 && lane == 0) {
+        const uint32_t r2 = t2 / G;
+        gp = __hip_atomic_load(&p.plocal[t2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        gr = r2 == 0 ? 0ull : __hip_atomic_load(&p.rprefix[r2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (lead)
+#pragma unroll
+        for (int j = 0; j < LPL; ++j)
+          la[j] = __hip_atomic_load(&p.granules[lvalid[j] ? lt + j : 0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    // ---- decode this tile (its words were loaded during the previous iteration) --------
+    const uint32_t seg0 = cur * (uint32_t)(U * TB) + (uint32_t)tid;
+    uint32_t ow[U][OW], cnt[U];
+    {
+      int start[U];
+      bool act[U];
+      uint32_t e[U][5];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t seg = seg0 + (uint32_t)(u * TB);
+        act[u] = have_cur && seg < nseg;
+        start[u] = seg == 0 ? (int)p.first_start : (int)gap_nib(gw[u], p.gap_nib0 + seg - 1u);
+        make_ewin(w[u], w4[u], start[u], S, e[u]);
+      }
+      if (have_cur) {
+        decode_tile_grouped<GRP, U, TILE_MIDG>(e, start, act, ow, cnt, amask, laneoff, mid);
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          cnt[u] = 0;
+#pragma unroll
+          for (int k2 = 0; k2 < OW; ++k2) ow[u][k2] = 0;
+        }
+        mid();
+      }
+    }
+    // ---- copy tile k-2 out (its prefix was published about an iteration ago) ----------
+    if (have2) {
+      unsigned long long goff = 0;
+      if (lane == 0) {
+        const uint32_t r2 = t2 / G;
+        if (!granule_ok(p, gp, 2)) {
+          if (wid == 0) atomicAdd(p.stats, 1ull);
+          gp = poll_granule(p, &p.plocal[t2], 2);
+        }
+        if (r2 > 0 && !granule_ok(p, gr, 2)) {
+          if (wid == 0) atomicAdd(p.stats + 1, 1ull);
+          gr = poll_granule(p, &p.rprefix[r2], 2);
+        }
+        goff = (gp & GRAN_VMASK) + (r2 > 0 ? (gr & GRAN_VMASK) : 0ull);
+        if (wid == 0 && t2 == p.ntiles - 1) *p.total = goff + tot2;
+      }
+      goff = rfl_u64(goff);
+      const uint32_t n2 = goff >= p.out_cap ? 0u : (uint32_t)min<unsigned long long>(tot2, p.out_cap - goff);
+      load(nxt);  // the next tile's words, issued before this copy-out's stores
+      copy_out_tile<TB, TILE_NS>(p.out, p.lut_bytes + buf * p.stage_bytes, goff, n2, tid,
+                                 p.junk + (unsigned long long)blockIdx.x * TB + tid);
+    } else {
+      load(nxt);
+    }
+    uint32_t bpos[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t incl = wave_incl_scan(cnt[u]);
+      if (lane == 63) s_wsum[(par * U + u) * NWAVE_T + wid] = incl;
+      bpos[u] = incl - cnt[u];
+    }
+    // leader: every aggregate of the round published?  (rarely not: poll)
+    uint32_t lval[LPL], lsum = 0, lincl = 0;
+    if (lead) {
+      bool ready = true;
+#pragma unroll
+      for (int j = 0; j < LPL; ++j) ready &= !lvalid[j] || granule_ok(p, la[j], 1) || granule_ok(p, la[j], 2);
+      if (!__all(ready)) {
+        if (lane == 0) atomicAdd(p.stats + 2, 1ull);
+#pragma unroll
+        for (int j = 0; j < LPL; ++j)
+          if (lvalid[j] && !(granule_ok(p, la[j], 1) || granule_ok(p, la[j], 2)))
+            la[j] = poll_granule(p, &p.granules[lt + j], 1);
+      }
+#pragma unroll
+      for (int j = 0; j < LPL; ++j) {
+        lval[j] = lvalid[j] ? (uint32_t)(la[j] & GRAN_VMASK) : 0u;  // a tile holds < 2^32 symbols
+        lsum += lval[j];
+      }
+      lincl = wave_incl_scan(lsum);
+      if (lane == 63) s_lead[wid] = lincl;
+    }
+    __syncthreads();  // tile sums, leader batch totals
+    uint32_t tile_total = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      uint32_t add = tile_total;
+#pragma unroll
+      for (int q = 0; q < NWAVE_T; ++q) {
+        const uint32_t x = s_wsum[(par * U + u) * NWAVE_T + q];
+        add += (q < wid) ? x : 0u;
+        tile_total += x;
+      }
+      bpos[u] += add;
+    }
+    tile_total = __builtin_amdgcn_readfirstlane(tile_total);
+    if (tid == 0 && have_cur)
+      __hip_atomic_store(&p.granules[cur], granule(p.epoch, 1, tile_total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lead) {  // publish the round's within-round prefixes and R[lr + 1]
+      unsigned long long before = 0, total = 0;
+#pragma unroll
+      for (int q = 0; q < LDR_NB; ++q) {
+        const uint32_t x = s_lead[q];
+        before += (q < wid) ? x : 0u;
+        total += x;
+      }
+      unsigned long long run = before + lincl - lsum;
+#pragma unroll
+      for (int j = 0; j < LPL; ++j) {
+        if (lvalid[j])
+          __hip_atomic_store(&p.plocal[lt + j], granule(p.epoch, 2, run), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        run += lval[j];
+      }
+      if (tid == 0) {
+        if (lr > 0 && !granule_ok(p, rl, 2)) {
+          atomicAdd(p.stats + 3, 1ull);
+          rl = poll_granule(p, &p.rprefix[lr], 2);
+        }
+        const unsigned long long r0 = lr > 0 ? (rl & GRAN_VMASK) : 0ull;
+        __hip_atomic_store(&p.rprefix[lr + 1], granule(p.epoch, 2, r0 + total), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (have_cur) {
+      // stage this tile into buffer k & 1 (copied out two iterations later) at its
+      // absolute LDS address (the kernel's LDS starts at 0)
+      const uint32_t sbase = p.lut_bytes + buf * p.stage_bytes + STAGE_PAD;
+      uint32_t nb[U], hv[U], ha[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        nb[u] = 0;
+        hv[u] = ow[u][0];
+        ha[u] = sbase + bpos[u];
+        if (cnt[u]) nb[u] = stage_aligned_p1(ow[u], cnt[u], ha[u]);
+      }
+      __syncthreads();  // phase 1 done: every segment's tail dword is in place
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (nb[u]) stage_head(ha[u], hv[u], nb[u]);
+    }
+    t2 = t1;
+    tot2 = tot1;
+    t1 = have_cur ? cur : NONE;
+    tot1 = tile_total;
+    buf ^= 1u;
+    cur = nxt < p.ntiles ? nxt : NONE;
+    nxt += G;
+  }
+}

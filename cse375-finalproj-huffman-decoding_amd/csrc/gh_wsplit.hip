@@ -1,21 +1,24 @@
-// Wave-independent split decode ("wsplit"), included by gh_decode.hip after
-// gh_msplit.hip (whose LUT format and per-lookup helpers it shares).
+// Wave split: the decode of every code that is not grouped (gh_tile.hip), included by
+// gh_decode.hip.  Reference counterpart: the count / scan / decode passes of
+// gpu_dec_l1_l2 (decoder/src/decoder.cu:529-728), whose segment rule is kept: segment i
+// decodes the codewords that start in [128i + gap[i-1], 128(i+1)).  Because gap[i] is the
+// end bit (minus 128) of the codeword crossing the boundary, those are exactly the
+// codewords lying wholly inside [start_i, E_i), E_i = 128 + gap[i] (segment-relative).
 //
-// Same code shapes as msplit (complete code, maxlen <= K <= 12, minlen >= 2: one K-bit
-// lookup yields up to four symbols), same two decode passes as the reference
-// (count, scan, decode again and write: decoder.cu:529-728), but with no workgroup
-// barrier and no inter-workgroup wait inside either decode pass.  The unit of work is
-// a wave block: U chains x 64 consecutive segments (lane l of chain u owns segment
-// 64u + l of the block).  The blocks are cut into `nranges` contiguous ranges
-// (range r = blocks [r*nb/R, (r+1)*nb/R)), one per wave of the write grid; a wave
-// of the count grid takes ranges w, w + W, ...  (An atomic ticket per block measured
-// ~0.4 ms per kernel on cfg2: one counter serves ~90 M tickets/s.  A scan over one
-// total per block was latency-bound: 363 K totals on cfg5.)
+// Two decode passes as in the reference, but no workgroup barrier and no
+// inter-workgroup wait inside either pass.  The unit of work is a wave block: U chains x
+// 64 consecutive segments (lane l of chain u owns segment 64u + l of the block).  The
+// blocks are cut into `nranges` contiguous ranges (range r = blocks [r*nb/R,
+// (r+1)*nb/R)), one per wave of the write grid; a wave of the count grid takes ranges w,
+// w + W, ...  (An atomic ticket per block measured ~0.4 ms per kernel on cfg2: one
+// counter serves ~90 M tickets/s.  A scan over one total per block was latency-bound:
+// 363 K totals on cfg5.)
 //
 //   gh_ws_count_kernel  counts the codewords of every segment (1 byte per segment)
 //                       and each range's symbol total;
 //   gh_ws_scan_kernel   one workgroup: exclusive scan of the range totals -> the
-//                       output offset of every range, and the stream total;
+//                       output offset of every range, and the stream total (replaces
+//                       the decoupled look-back, decoder.cu:571-653);
 //   gh_ws_write_kernel  decodes each block again, ORs every lookup's four symbol bytes
 //                       into the wave's own LDS staging at the scanned offset, and
 //                       copies the block out with 16-byte stores aligned to the
@@ -23,11 +26,9 @@
 //
 // A wave never waits for another wave: it scans its block's counts with DPP, stages
 // and copies out alone (LDS operations of one wave complete in order), and its stores
-// drain while it decodes the next block.
-//
-// Reference counterpart: the count / scan / decode passes of gpu_dec_l1_l2
-// (decoder.cu:529-728) and its decoupled look-back (:571-653), replaced here by the
-// block-total scan.
+// drain while it decodes the next block.  The tables (gh_lut.hpp) hold up to four
+// codewords per write lookup; codewords longer than a table and patterns outside an
+// incomplete code go through the canonical fallback (template parameter FB).
 
 #ifndef GH_WS_TB
 #define GH_WS_TB 512
@@ -44,9 +45,6 @@ constexpr int WS_U = 2;     // chains per lane of the write kernel (segments per
 constexpr int WS_UC = GH_WS_UC;  // chains per lane of the count kernel
 constexpr int WS_SB = 256;  // segments per superblock: ranges are cut at superblock edges
 constexpr int WS_SCAN_TB = 1024;
-#ifndef GH_WS_BF
-#define GH_WS_BF 1  // branch-free staging: every lane ORs (zero past its end), one 64-bit shift per lookup
-#endif
 #ifndef GH_WS_PRIO
 #define GH_WS_PRIO 4  // rotate s_setprio over 4 workgroup slots by block (0: off); cfg3 0.579 -> 0.565 ms
 #endif
@@ -67,14 +65,11 @@ constexpr int WS_SCAN_TB = 1024;
 #else
 #define WS_PRIO(blk, b, g) do {} while (0)
 #endif
-#ifndef GH_WS_ABLATE
-#define GH_WS_ABLATE 0  // diagnostic builds only (results wrong): 1 no LDS OR, 2 no stores, 4 no copy-out
-#endif
 
 struct WsParams {
   const uint32_t* payload;         // local segment j owns words [4j, 4j+4); +1 look-ahead, zero padded
   const uint32_t* gaps;            // nibble gap_nib0 + j - 1: start of segment j >= 1; gap_nib0 + j: its end
-  const uint2* lut;                // count: {b, end mask}; write: {symbols, b | n << 8}; 2^K entries
+  const uint2* lut;                // count: u32 {b | end mask << 16}; write: u64 {symbols, b | n << 8}
   uint8_t* seg_cnt;                // codewords per segment
   unsigned long long* rng_tot;     // symbols per range
   unsigned long long* rng_off;     // output offset per range (scan kernel)
@@ -162,19 +157,6 @@ __device__ __forceinline__ void ws_fb_to_lds(const WsParams& p, uint32_t* s_fb, 
   for (uint32_t i = tid; i < (uint32_t)FB_WORDS; i += TBK) s_fb[i] = p.fb[i];
 }
 
-// Count-LUT lookup results: ds_read_b32 each, one wait for the U of a step.
-template <int U>
-__device__ __forceinline__ void ws_wait32(uint32_t (&v)[U]) {
-  static_assert(U == 1 || U == 2 || U == 4, "ws_wait32: 1, 2 or 4 lookups");
-  if constexpr (U == 1) {
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0])::"memory");
-  } else if constexpr (U == 2) {
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1])::"memory");
-  } else {
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3])::"memory");
-  }
-}
-
 // The count kernel's LUT (its own width Kc <= 14, u32 entries, 4 << Kc bytes): entry
 // = b | endmask << 16, b = bits of the complete codewords in the Kc-bit window (all
 // of them, no cap), end-mask bit e-1 per codeword end e.  One lookup step:
@@ -216,9 +198,9 @@ __global__ __launch_bounds__(TBK) void gh_ws_count_kernel(const WsParams p) {
       for (int u = 0; u < U; ++u) {
         const uint32_t seg = blk * (uint32_t)(64 * U) + (uint32_t)(64 * u + lane);
         act[u] = seg < p.nseg;
-        const int start = seg == 0 ? (int)p.first_start : (int)ms_nib(ga[u], p.gap_nib0 + seg - 1u);
+        const int start = seg == 0 ? (int)p.first_start : (int)gap_nib(ga[u], p.gap_nib0 + seg - 1u);
         const int E = (p.last_end && seg == p.nseg - 1u) ? (int)p.last_end
-                                                         : 128 + (int)ms_nib(gb[u], p.gap_nib0 + seg);
+                                                         : 128 + (int)gap_nib(gb[u], p.gap_nib0 + seg);
         v[u] = make_win(w[u], w4[u], start);
         R[u] = act[u] ? E - start : 0;
         cnt[u] = 0;
@@ -240,7 +222,7 @@ __global__ __launch_bounds__(TBK) void gh_ws_count_kernel(const WsParams p) {
             xs[u] = x;
             asm volatile("ds_read_b32 %0, %1" : "=v"(e[u]) : "v"((x >> sh) & amask) : "memory");
           }
-          ws_wait32(e);
+          lds_wait(e);
   #pragma unroll
           for (int u = 0; u < U; ++u) {
             if constexpr (FB) {
@@ -260,7 +242,7 @@ __global__ __launch_bounds__(TBK) void gh_ws_count_kernel(const WsParams p) {
         bool more = false;
   #pragma unroll
         for (int u = 0; u < U; ++u) {
-          ms_shift(v[u], q[u]);  // consumed = 32 - (q & 0xFFFF), 2..32: v_alignbit reads q & 31
+          win_shift(v[u], q[u]);  // consumed = 32 - (q & 0xFFFF), 2..32: v_alignbit reads q & 31
           R[u] -= 32 - (int)(q[u] & 0xFFFFu);
           more |= R[u] > 0;
         }
@@ -308,6 +290,14 @@ __global__ __launch_bounds__(WS_SCAN_TB) void gh_ws_scan_kernel(const WsParams p
     run += t;
   }
   if (tid == 0) *p.total = all;
+}
+
+// ptr += byte 1 of meta (n, the lookup's symbols): one SDWA add.
+__device__ __forceinline__ uint32_t add_n(uint32_t ptr, uint32_t meta) {
+  uint32_t r;
+  asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1"
+      : "=v"(r) : "v"(ptr), "v"(meta));
+  return r;
 }
 
 // OR the four bytes v at LDS byte address a (any alignment) into the two aligned
@@ -388,7 +378,7 @@ __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const uint32_t seg = blk * (uint32_t)(64 * U) + (uint32_t)(64 * u + lane);
-        start[u] = seg == 0 ? (int)p.first_start : (int)ms_nib(ga[u], p.gap_nib0 + seg - 1u);
+        start[u] = seg == 0 ? (int)p.first_start : (int)gap_nib(ga[u], p.gap_nib0 + seg - 1u);
         cc[u] = seg < p.nseg ? c8[u] : 0u;
       }
       uint4 wc[U];
@@ -407,7 +397,7 @@ __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
       uint32_t bpos[U], ctot[U], coff[U], btot = 0;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const uint32_t incl = wave_incl_scan(cc[u], lane);
+        const uint32_t incl = wave_incl_scan(cc[u]);
         bpos[u] = incl - cc[u];
         ctot[u] = __builtin_amdgcn_readlane(incl, 63);
         coff[u] = btot;
@@ -442,9 +432,9 @@ __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
             for (int u = 0; u < U; ++u) {
               const uint32_t x = j == 0 ? v[u].d0 : __builtin_amdgcn_alignbit(v[u].d0, v[u].d1, q[u]);
               xs[u] = x;
-              e[u] = ms_lds_u64((x >> sh) & amask);
+              e[u] = lds_u64_nowait((x >> sh) & amask);
             }
-            ms_wait(e);
+            lds_wait(e);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
               if constexpr (FB) {
@@ -453,21 +443,18 @@ __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
                   e[u] = make_uint2(r >> 8, (r & 31u) | (1u << 8));
                 }
               }
-              if constexpr (GH_WS_BF) {
-                // a lane past its end ORs zero at its end (inside the staging spill)
+              {  // branch-free: a lane past its end ORs zero at its end (inside the staging spill)
                 const bool on = ptr[u] < end[u];
-                if (!(GH_WS_ABLATE & 1)) ws_lds_or4(on ? ptr[u] : end[u], on ? e[u].x : 0u);
-              } else if (!(GH_WS_ABLATE & 1) && ptr[u] < end[u]) {
-                ms_lds_or_bytes(ptr[u], e[u].x);
+                ws_lds_or4(on ? ptr[u] : end[u], on ? e[u].x : 0u);
               }
-              ptr[u] = ms_add_n(ptr[u], e[u].y);
+              ptr[u] = add_n(ptr[u], e[u].y);
               q[u] -= e[u].y;
             }
           }
           bool more = false;
 #pragma unroll
           for (int u = 0; u < U; ++u) {
-            ms_shift(v[u], q[u]);
+            win_shift(v[u], q[u]);
             more |= ptr[u] < end[u];
           }
           if (!__any(more)) break;
@@ -482,12 +469,12 @@ __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
         const uint32_t cend = ((lb + hb) >> 4) + 1u;  // chunks [1, cend) end inside the piece
         uint32_t c_lo = 1;
         if (hs != 0 && cend > 1u) {  // the range's first chunk is complete: its bytes [hs, 16)
-          if (!(GH_WS_ABLATE & 2) && WS_CK(a0 + 16 <= p.chk_out || !GH_WS_CHECK, 0x1000))
+          if (WS_CK(a0 + 16 <= p.chk_out || !GH_WS_CHECK, 0x1000))
             ws_store_bytes(p.out + a0, st4 + 1, hs, 16u, lane);
           c_lo = 2;
           hs = 0;
         }
-        if (!(GH_WS_ABLATE & 4)) {
+        {
           // padding stores rewrite the piece's last complete chunk (same bytes: the
           // duplicate merges in L2 instead of costing an HBM write); the junk slot only
           // when the piece has no complete chunk
@@ -500,17 +487,17 @@ __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
             const uint32_t cs = real ? c : cdup;
             const uint4 d = st4[cs];
             uint4* dst = (real || have) ? (uint4*)(p.out + a0 - 16 + 16ull * cs) : junk;
-            if (!(GH_WS_ABLATE & 2) && WS_CK(!real || a0 + 16ull * c <= p.chk_out || !GH_WS_CHECK, 0x2000)) *dst = d;
+            if (WS_CK(!real || a0 + 16ull * c <= p.chk_out || !GH_WS_CHECK, 0x2000)) *dst = d;
           }
           for (uint32_t c = c_lo + (uint32_t)lane + 64u * NS; c < cend; c += 64u)
-            if (!(GH_WS_ABLATE & 2) && WS_CK(a0 + 16ull * c <= p.chk_out || !GH_WS_CHECK, 0x4000))
+            if (WS_CK(a0 + 16ull * c <= p.chk_out || !GH_WS_CHECK, 0x4000))
               *(uint4*)(p.out + a0 - 16 + 16ull * c) = st4[c];
         }
         if (goff + hbytes >= p.out_cap) {
           // the output ends in this piece: its partial last chunk (staging chunk cend,
           // output bytes [out_cap & ~15, out_cap)) now, and no later piece writes
           const uint32_t te = (uint32_t)(p.out_cap & 15);
-          if (te != 0 && p.out_cap > rs && !(GH_WS_ABLATE & 2) && WS_CK(p.out_cap <= p.chk_out || !GH_WS_CHECK, 0x8000))
+          if (te != 0 && p.out_cap > rs && WS_CK(p.out_cap <= p.chk_out || !GH_WS_CHECK, 0x8000))
             ws_store_bytes(p.out + (p.out_cap - te), st4 + cend, cend == 1 ? hs : 0u, te, lane);
           capped = true;
           break;
@@ -530,7 +517,7 @@ __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
   if (b0 < b1 && !capped) {
     const unsigned long long ge = min(goff, p.out_cap);
     const uint32_t te = (uint32_t)(ge & 15);
-    if (te != 0 && ge > rs && !(GH_WS_ABLATE & 2) && WS_CK(ge <= p.chk_out || !GH_WS_CHECK, 0x8000))
+    if (te != 0 && ge > rs && WS_CK(ge <= p.chk_out || !GH_WS_CHECK, 0x8000))
       ws_store_bytes(p.out + (ge - te), st4 + 1, hs, te, lane);
   }
   if (FB && __any(bad != 0) && lane == 0) atomicOr(p.status, (unsigned)GH_ST_BADCODE);

@@ -105,8 +105,8 @@ class gh_sync_report(ctypes.Structure):
                 ("kernel_ms", ctypes.c_float)]
 
 
-MODE_NAMES = {0: "fused", 1: "split", 2: "tile"}
-PATH_NAMES = {0: "multi", 1: "single", 2: "grouped", 3: "multi_lean", 4: "multi_wave"}
+MODE_NAMES = {1: "split", 2: "tile"}
+PATH_NAMES = {2: "grouped", 4: "multi_wave"}
 
 
 class gh_opts(ctypes.Structure):

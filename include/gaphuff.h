@@ -143,26 +143,22 @@ typedef struct gh_report {
   uint64_t symbols;        /* symbols decoded by the loaded shard (incl. padding)  */
   uint64_t out_bytes;      /* bytes written to the shard's device output           */
   uint32_t status;         /* device status bits (GH_ST_*)                          */
-  uint32_t lut_bits;       /* K of the multi-symbol lookup table                    */
+  uint32_t lut_bits;       /* K of the decode lookup table (write table: wave split) */
   uint32_t grid;           /* workgroups launched (write kernel in split mode)      */
   uint32_t tiles;          /* segment tiles in the shard                            */
   float kernel_ms;         /* average time of one decode (all its kernels), events  */
   uint32_t launches;       /* decodes averaged in kernel_ms                         */
-  uint32_t mode;           /* GH_MODE_FUSED, GH_MODE_SPLIT or GH_MODE_TILE          */
+  uint32_t mode;           /* GH_MODE_SPLIT or GH_MODE_TILE                         */
   uint32_t path;           /* GH_PATH_*: table / decode-loop variant                */
-  uint64_t slow_lookbacks; /* tile mode: look-backs that needed the slow path        */
+  uint64_t slow_lookbacks; /* tile mode: prefix reads that had to poll              */
 } gh_report;
 
-#define GH_MODE_FUSED 0u    /* one persistent kernel, decoupled look-back            */
-#define GH_MODE_SPLIT 1u    /* count kernel + write kernel                           */
-#define GH_MODE_TILE 2u     /* persistent tile kernel, look-back per tile            */
-#define GH_PATH_MULTI 0u    /* multi-symbol LUT, count + emit passes                 */
-#define GH_PATH_SINGLE 1u   /* single-symbol LUT, one pass (fallback for long codes) */
-#define GH_PATH_GROUPED 2u  /* single-symbol LUT, grouped window shifts              */
-#define GH_PATH_MULTI_LEAN 3u /* multi-symbol LUT (complete code, maxlen <= 12):
-                                 end-mask count kernel + unaligned-store write kernel */
-#define GH_PATH_MULTI_WAVE 4u /* multi-symbol LUT, wave-independent count / scan / write
-                                 kernels (no barriers, ranges by ticket) */
+#define GH_MODE_SPLIT 1u    /* wave split: count, scan and write kernels (gh_wsplit.hip) */
+#define GH_MODE_TILE 2u     /* persistent tile kernel, round-leader prefixes (gh_tile.hip) */
+#define GH_PATH_GROUPED 2u  /* one codeword per lookup, grouped window shifts (tile kernel) */
+#define GH_PATH_MULTI_WAVE 4u /* up to four codewords per lookup, canonical fallback for
+                                 longer or incomplete codes (wave split) */
+/* (values 0, 1, 3 were retired structures; they are no longer reported) */
 
 #define GH_ST_BADCODE 1u    /* a bit pattern outside the code space was met       */
 #define GH_ST_TIMEOUT 2u    /* look-back spin gave up (never expected)            */

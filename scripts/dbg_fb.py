@@ -11,7 +11,7 @@ for q in (0.5, 0.7):
     img = gh.encode(data); s = gh.parse(img)
     lens = [l for _, l in s.symbols]
     counts = np.array([oracle.segment_count(img, i) for i in range(s.g)])
-    for env in ("", "GH_WS_KC=16", "GH_MS_K=12"):
+    for env in ("", "GH_WS_KC=16", "GH_WS_K=12"):
         for kv in env.split():
             k, v = kv.split("="); os.environ[k] = v
         with gh.Decoder(0) as d:

@@ -6,6 +6,6 @@ O=gpurun_out/lc; mkdir -p $O
 export TMPDIR=/tmp
 step ws 300 $O/ws.txt rocprofv3 --kernel-trace --stats -d $O/ws -o ws -- python3 -u scripts/time_longcodes.py --n 1000000000
 cat $O/ws.txt
-GH_MODE=msplit step ms 300 $O/ms.txt rocprofv3 --kernel-trace --stats -d $O/ms -o ms -- python3 -u scripts/time_longcodes.py --n 1000000000
-cat $O/ms.txt
+
+
 find $O -name "*kernel_stats.csv" | while read f; do echo "== $f"; cut -d, -f1-4 "$f" | head -8; done

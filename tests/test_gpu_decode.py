@@ -153,46 +153,40 @@ def test_config_1GB_bitexact(gpu, cfg):
     assert np.array_equal(out, data)
 
 
-@pytest.mark.parametrize("mode", ["fused", "split"])
-@pytest.mark.parametrize("path", ["1", "2", "3"])
-@pytest.mark.parametrize("u", ["1", "2", "4"])
-def test_decode_paths_and_ilp(gpu, orc, path, u, mode, monkeypatch):
-    """Every decode path (1 = single-pass single-symbol, grouped window shifts when
-    the code is complete and fits the LUT; 2 = count + emit with multi-symbol
-    lookups; 3 = single-pass single-symbol without grouping) and every ILP width
-    give identical bytes, in both the fused persistent kernel and the split
-    count / write kernels."""
+@pytest.mark.parametrize("mode", ["tile", "wsplit"])
+def test_both_structures_on_grouped_codes(gpu, orc, mode, monkeypatch):
+    """Grouped codes (complete, 4..12-bit codewords) decode to the same bytes through
+    the tile kernel and through the wave split (GH_MODE), and so do codes the tile
+    kernel does not take (codewords up to 16 bits: the wave split's canonical
+    fallback)."""
     monkeypatch.setenv("GH_MODE", mode)
-    monkeypatch.setenv("GH_PATH", path)
-    monkeypatch.setenv("GH_U", u)
     cases = [gpu.generate(21, 0.1, 300_001), gpu.generate(22, 0.0, 77_777)]
     x = np.tile(np.arange(256, dtype=np.uint8), 300)
     np.random.default_rng(2).shuffle(x)
     cases.append(x)
-    counts = [max(1, int(2 ** (15 - 0.35 * i))) for i in range(40)]
-    g = np.repeat(np.arange(40, dtype=np.uint8) + 60, counts)
-    np.random.default_rng(4).shuffle(g)
-    cases.append(g)  # minlen >= 4 with long codes -> fallback inside path 1
     for d in cases:
-        _roundtrip(gpu, orc, d)
-
-
-@pytest.mark.parametrize("mode", ["fused", "split"])
-def test_dynamic_ticket_schedule(gpu, orc, mode, monkeypatch):
-    """The fused kernel's atomic-ticket tile schedule (GH_SCHED=dynamic) decodes the
-    same bytes as the default static schedule; repeated launches reuse the ticket."""
-    monkeypatch.setenv("GH_SCHED", "dynamic")
-    monkeypatch.setenv("GH_MODE", mode)
-    for r in (0.1, 0.5, 0.9):
-        data = gpu.generate(77, r, 2_000_003)
-        img = gpu.encode(data)
+        img = _roundtrip(gpu, orc, d)
+        with gpu.Decoder(0) as dec:
+            dec.load(gpu.parse(img))
+            dec.decode()
+            rep = dec.report()
+        assert gpu.PATH_NAMES[rep.path] == ("grouped" if mode == "tile" else "multi_wave")
+    if mode == "wsplit":
+        counts = [max(1, int(2 ** (15 - 0.35 * i))) for i in range(40)]
+        g = np.repeat(np.arange(40, dtype=np.uint8) + 60, counts)
+        np.random.default_rng(4).shuffle(g)
+        img = _roundtrip(gpu, orc, g)
         s = gpu.parse(img)
-        with gpu.Decoder(0) as d:
+        assert max(l for _, l in s.symbols) > 12
+
+
+def test_tile_mode_refuses_other_codes(gpu, monkeypatch):
+    """GH_MODE=tile on a code the tile kernel does not take fails loudly at load."""
+    monkeypatch.setenv("GH_MODE", "tile")
+    s = gpu.parse(gpu.encode(gpu.generate(23, 0.9, 100_000)))
+    with gpu.Decoder(0) as d:
+        with pytest.raises(gpu.GapHuffError):
             d.load(s)
-            for _ in range(3):
-                d.decode()
-            assert d.report().status == 0
-            assert np.array_equal(d.download(s.n), data)
 
 
 @pytest.mark.gpu
@@ -224,24 +218,19 @@ def test_graft_smoke(gpu):
 
 @pytest.mark.parametrize("k", ["", "10", "11", "12"])
 @pytest.mark.parametrize("stage", ["", "1"])
-@pytest.mark.parametrize("wu", ["", "1", "2", "ws", "ws1", "ws3"])  # "wsN": GH_WS_GRID=N
-def test_lean_split_widths_and_staging(gpu, orc, k, stage, wu, monkeypatch):
-    """The multi-symbol split kernels at every LUT width, with the default staging and
+@pytest.mark.parametrize("grid", ["", "1", "3"])
+def test_wave_split_widths_and_staging(gpu, orc, k, stage, grid, monkeypatch):
+    """The wave split at every write-LUT width (GH_WS_K), with the default staging and
     with the staging forced down to one chain's worst case, so that blocks are staged
-    one chain at a time (GH_MS_STAGE).  wu "", "1", "2": the workgroup-tile kernels
-    (gh_msplit.hip) with either write geometry (GH_MS_WU: one chain per thread x 512,
-    or two x 256); "ws*": the wave-independent kernels (gh_wsplit.hip) on the default
-    grid and on grids of 1 and 3 workgroups (GH_WS_GRID: each wave walks many blocks)."""
-    ws = wu.startswith("ws")
-    monkeypatch.setenv("GH_MODE", "wsplit" if ws else "msplit")
-    if ws and wu[2:]:
-        monkeypatch.setenv("GH_WS_GRID", wu[2:])
-    if wu and not ws:
-        monkeypatch.setenv("GH_MS_WU", wu)
+    one chain at a time (GH_WS_STAGE), on the default grid and on grids of 1 and 3
+    workgroups (GH_WS_GRID: each wave walks many blocks)."""
+    monkeypatch.setenv("GH_MODE", "wsplit")
+    if grid:
+        monkeypatch.setenv("GH_WS_GRID", grid)
     if k:
-        monkeypatch.setenv("GH_MS_K", k)
+        monkeypatch.setenv("GH_WS_K", k)
     if stage:
-        monkeypatch.setenv("GH_MS_STAGE", stage)
+        monkeypatch.setenv("GH_WS_STAGE", stage)
     for seed, r, n in ((31, 0.9, 700_001), (32, 0.5, 400_003), (33, 0.999, 65_549), (34, 0.1, 9_999)):
         data = gpu.generate(seed, r, n)
         img = _roundtrip(gpu, orc, data)
@@ -250,20 +239,18 @@ def test_lean_split_widths_and_staging(gpu, orc, k, stage, wu, monkeypatch):
             d.load(s)
             d.decode()
             rep = d.report()
-        if max(l for _, l in s.symbols) <= 12:
-            assert gpu.PATH_NAMES[rep.path] == ("multi_wave" if ws else "multi_lean")
+        assert gpu.PATH_NAMES[rep.path] == "multi_wave"
         total = sum(orc.segment_count(img, i) for i in range(s.g)) if n < 100_000 else None
         if total is not None:
             assert rep.symbols == total
 
 
-@pytest.mark.parametrize("mode", ["msplit", "wsplit"])
-def test_lean_split_shard_counts(gpu, orc, mode, monkeypatch):
-    """Shards through the multi-symbol split kernels: per-shard symbol counts equal the
-    reference segment rule's (decoder.cu:529-569), including the stream's last
-    segment (its zero padding, last_segment_end)."""
-    monkeypatch.setenv("GH_MODE", mode)
-    data = gpu.generate(35, 0.5, 250_000)
+@pytest.mark.parametrize("r", [0.5, 0.1])
+def test_shard_counts_both_structures(gpu, orc, r):
+    """Shards through the default structure (r=0.5: wave split, r=0.1: tile kernel):
+    per-shard symbol counts equal the reference segment rule's (decoder.cu:529-569),
+    including the stream's last segment (its zero padding, last_segment_end)."""
+    data = gpu.generate(35, r, 250_000)
     img = gpu.encode(data)
     s = gpu.parse(img)
     bounds = gpu.plan_shards(s.g, 4)
@@ -272,12 +259,12 @@ def test_lean_split_shard_counts(gpu, orc, mode, monkeypatch):
         with gpu.Decoder(0) as d:
             d.load(s, bounds[k], bounds[k + 1])
             d.decode()
-            r = d.report()
+            r_ = d.report()
             expect = sum(orc.segment_count(img, i) for i in range(bounds[k], bounds[k + 1]))
-            assert r.symbols == expect and r.status == 0
-            keep = min(r.symbols, s.n - off)
+            assert r_.symbols == expect and r_.status == 0
+            keep = min(r_.symbols, s.n - off)
             assert np.array_equal(d.download(keep), data[off:off + keep])
-            off += r.symbols
+            off += r_.symbols
 
 
 @pytest.mark.parametrize("mode", ["tile"])
