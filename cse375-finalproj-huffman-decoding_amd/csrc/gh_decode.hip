@@ -185,8 +185,11 @@ static int tile_setup(gh_ctx* c, uint32_t K) {
   c->lgr = (uint32_t)best_lg;
   c->lut_bytes = 4ull << (K + best_lg);
   c->lds = tile_lds_bytes(c->lut_bytes, c->stage_bytes);
-  // a round's aggregates are read by its leader, one per lane: grid <= TILE_TB
-  c->grid = (uint32_t)std::min<uint64_t>({(uint64_t)c->ntiles, (uint64_t)best * c->num_cu, (uint64_t)TILE_TB});
+  // workgroup 0 leads the rounds (one aggregate per thread: D = grid - 1 < TILE_TB), the
+  // others decode; every workgroup must be resident at once (the grid is sized from the
+  // occupancy; decodes on one device are chained, see DevChain)
+  c->grid = (uint32_t)std::min<uint64_t>({(uint64_t)c->ntiles + 1, (uint64_t)best * c->num_cu, (uint64_t)TILE_TB});
+  if (c->grid < 2) return GH_OK;  // (the wave split then takes the code)
   GH_HIP(hipMalloc(&c->d_tile_junk, 16ull * c->grid * TILE_TB));
   c->tile = true;
   return GH_OK;
@@ -437,8 +440,8 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
     }
     if (!c->tile && (rc = ws_setup(c, s->g ? (double)s->n / (double)s->g : 16.0))) return rc;
   }
-  // tile kernel: per-tile aggregates and within-round prefixes, per-round starts
-  c->gran_words = c->tile ? 2ull * c->ntiles + ceil_div(c->ntiles, std::max<uint32_t>(c->grid, 1)) + 2 : 1;
+  // tile kernel: per-tile aggregates and prefixes
+  c->gran_words = c->tile ? 2ull * c->ntiles + 2 : 1;
   GH_HIP(hipMalloc(&c->d_gran, 8ull * c->gran_words));
   GH_HIP(hipMemset(c->d_gran, 0, 8ull * c->gran_words));
   // start bit of local segment 0, and the gap nibble base for the rest
@@ -651,8 +654,7 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     t.lut = c->d_lut_t;
     t.out = c->d_out;
     t.granules = c->d_gran;
-    t.plocal = c->d_gran + c->ntiles;
-    t.rprefix = c->d_gran + 2ull * c->ntiles;
+    t.prefix = c->d_gran + c->ntiles;
     t.status = c->d_misc + 1;
     t.total = (unsigned long long*)(c->d_misc + 2);
     t.stats = (unsigned long long*)(c->d_misc + 4);

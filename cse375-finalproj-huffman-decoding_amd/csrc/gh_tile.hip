@@ -5,26 +5,31 @@
 // decode pass per segment in one persistent kernel.
 //
 // 512-thread workgroups, two segments per lane, a tile = 1024 consecutive segments.
-// Workgroup b takes tiles b, b + G, b + 2G, ... (static round robin over the G resident
-// workgroups; grid <= 512).  Iteration k of a workgroup:
+// Workgroup 0 is the round leader; the D = grid - 1 others decode: workgroup b takes
+// tiles b, b + D, b + 2D, ... (static round robin; grid <= 512).  Iteration k of a
+// decoding workgroup:
 //
 //   decode tile k into registers (one codeword per lookup, G codewords per window shift;
 //     a codeword is kept iff it starts before the segment end: the reference's rule)
-//     - mid-decode: load the prefix of tile k-2, and, as the round leader, the round's
-//       aggregates
+//     - mid-decode: load the global prefix of tile k-2
 //   copy tile k-2 out of staging (its prefix has had an iteration to arrive), with a
 //     fixed store count; the next tile's loads are issued just before
-//   wave scans of the counts -> BARRIER -> publish tile k's aggregate; the leader
-//     publishes its round's within-round prefixes and the next round's start
+//   wave scans of the counts -> BARRIER -> publish tile k's aggregate
 //   stage tile k (aligned dword stores, a second barrier, the 1-3 head bytes)
 //
-// Rounds and leaders: tile rG + j is decoded in iteration r by workgroup j.  Round r's
-// leader is the workgroup that decoded tile rG + (r mod n_r); in iteration r+1 it reads
-// the round's G aggregates (one per lane, issued mid-decode), scans them and publishes
-// every tile's within-round prefix (plocal) and R[r+1] = R[r] + the round's total.  The
-// owner of a tile reads R[round] + plocal[tile] one iteration later.  Every hand-off has
-// about an iteration of slack; a decoupled look-back with 512 tiles in flight needed a
-// window of ~512 granules per tile and mostly took its slow path.
+// The leader takes the rounds (tiles rD .. rD + D - 1) in order: it waits for a round's
+// aggregates, scans them and publishes every tile's global exclusive prefix.  The start
+// of the next round stays in its registers, so the serial chain of round starts never
+// crosses workgroups (rotating the leader role among the decoding workgroups made every
+// round pay one cross-workgroup hand-off on that chain: 0.73 vs 0.70 ms on cfg4).  A
+// decoupled look-back with 512 tiles in flight needed a window of ~512 granules per tile
+// and mostly took its slow path.
+//
+// Issue priority: the second workgroup dispatched to a CU loses issue-arbitration ties to
+// the first (age order), so one slot runs ~30 % slower and the other waits for its
+// prefixes.  A wave whose last prefix had to be polled is ahead of the grid and drops to
+// priority 0; one that found it published is behind and takes priority 2 (cfg4 0.70 ->
+// 0.68 ms; alternating the two slots' priority by iteration gave 0.747 -> 0.729 ms).
 
 constexpr int TILE_TB = 512;       // threads per workgroup
 constexpr int TILE_U = 2;          // segments per lane
@@ -39,8 +44,7 @@ struct TileParams {
   const uint32_t* lut;           // 2^K u32 {len | sym << 24}
   uint8_t* out;
   unsigned long long* granules;  // one per tile: its symbol count (flag 1)
-  unsigned long long* plocal;    // one per tile: exclusive prefix within its round (flag 2)
-  unsigned long long* rprefix;   // one per round: its starting offset (flag 2); [0] unused
+  unsigned long long* prefix;    // one per tile: its global exclusive prefix (flag 2, by the leader)
   unsigned int* status;
   unsigned long long* total;
   unsigned long long* stats;     // poll counters (reported as slow_lookbacks)
@@ -52,7 +56,7 @@ struct TileParams {
   uint4* junk;                   // 16 bytes per thread of the grid for padding stores
 };
 
-// LDS of the tile kernel: LUT, two staging buffers, wave sums, leader batch totals.
+// LDS of the tile kernel: LUT, two staging buffers, wave sums, leader wave totals.
 inline size_t tile_lds_bytes(size_t lut_bytes, size_t stage_bytes) {
   return lut_bytes + 2 * stage_bytes + 2 * (TILE_TB / 64) * 4 * TILE_U + 4 * (TILE_TB / 64) + 32;
 }
@@ -261,19 +265,59 @@ __device__ __forceinline__ unsigned long long poll_granule(const TileParams& p, 
   }
 }
 
-// TB threads, U segments per lane, GRP codewords per window shift.  Compiled for at
-// most 4 waves per SIMD (two workgroups per CU: 128 VGPRs).
+// The round leader (workgroup 0): for every round r of D = grid - 1 tiles, wait for the
+// round's aggregates (one per thread), scan them and publish each tile's global
+// exclusive prefix; R, the start of the round, stays in a register.  (Spreading the
+// rounds over the leader's waves, eight rounds' loads in flight, measured slower.)
+template <int TB>
+__device__ __forceinline__ void tile_round_leader(const TileParams& p, uint32_t* s_lead, int tid, int lane, int wid) {
+  const uint32_t D = gridDim.x - 1;
+  const uint32_t nr = (p.ntiles + D - 1) / D;
+  unsigned long long R = 0;
+  for (uint32_t r = 0; r < nr; ++r) {
+    const uint32_t t0 = r * D, n = min(D, p.ntiles - t0);
+    uint32_t v = 0;
+    if ((uint32_t)tid < n) {
+      unsigned long long g = __hip_atomic_load(&p.granules[t0 + tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (!granule_ok(p, g, 1)) {
+        atomicAdd(p.stats + 1, 1ull);
+        g = poll_granule(p, &p.granules[t0 + tid], 1);
+      }
+      v = (uint32_t)(g & GRAN_VMASK);  // a tile holds < 2^32 symbols
+    }
+    const uint32_t incl = wave_incl_scan(v);
+    if (lane == 63) s_lead[wid] = incl;
+    __syncthreads();
+    unsigned long long before = 0, total = 0;
+#pragma unroll
+    for (int q = 0; q < TB / 64; ++q) {
+      const uint32_t x = s_lead[q];
+      before += (q < wid) ? x : 0u;
+      total += x;
+    }
+    if ((uint32_t)tid < n)
+      __hip_atomic_store(&p.prefix[t0 + tid], granule(p.epoch, 2, R + before + incl - v), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    R += total;
+    __syncthreads();
+  }
+}
+
+// TB threads, U segments per lane, GRP codewords per window shift.  Compiled for at most
+// 4 waves per SIMD (two workgroups per CU: 128 VGPRs).
 template <int TB, int U, int GRP>
 __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void gh_tile_kernel(const TileParams p) {
   constexpr int NWAVE_T = TB / 64;
-  constexpr int LDR_NB = TB / 64;                  // leader batches: one wave per 64 * LPL tiles of a round
-  constexpr int LPL = TB >= 512 ? 1 : 1024 / TB;   // aggregates per leader lane (grid <= LPL * TB)
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* s_stage = smem + p.lut_bytes;                        // 2 buffers
   uint32_t* s_wsum = (uint32_t*)(s_stage + 2 * p.stage_bytes);  // [2][U][NWAVE_T]
-  uint32_t* s_lead = s_wsum + 2 * U * NWAVE_T;                  // [LDR_NB]
+  uint32_t* s_lead = s_wsum + 2 * U * NWAVE_T;                  // [NWAVE_T] (leader)
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (blockIdx.x == 0) {
+    tile_round_leader<TB>(p, s_lead, tid, lane, wid);
+    return;
+  }
   {  // LUT to LDS, replicated: dword i of LDS = entry i >> lgr (lane l reads copy l mod 2^lgr,
      // so up to 32 lanes of a ds_read_b32 hit distinct banks)
     const uint32_t nd = p.lut_bytes >> 2;
@@ -286,12 +330,9 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
   check_lds_base(smem, p.status);
   __syncthreads();
 
-  const uint32_t G = gridDim.x, b = blockIdx.x;  // grid size, workgroup
-  const uint32_t nseg = (uint32_t)p.nseg;         // < 2^31 (checked by the host)
+  const uint32_t G = gridDim.x - 1, b = blockIdx.x - 1;  // decoding workgroups, this one
+  const uint32_t nseg = (uint32_t)p.nseg;                 // < 2^31 (checked by the host)
   constexpr uint32_t NONE = 0xFFFFFFFFu;
-  // Static round robin (a dynamic ticket order can deadlock here: a workgroup waiting
-  // for its tile's prefix may hold an undecoded tile of the same round, whose leader then
-  // waits for it).
   const uint32_t last_tile_k = b < p.ntiles ? (p.ntiles - 1 - b) / G : NONE;
   uint32_t cur = b, nxt = b + G;
   uint4 w[U];
@@ -311,49 +352,24 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
   uint32_t t1 = NONE, t2 = NONE;  // tiles of iterations k-1, k-2
   uint32_t tot1 = 0, tot2 = 0;    // their totals
   uint32_t buf = 0;               // k & 1
+  bool ahead = false;             // the last prefix had to be polled
   for (uint32_t k = 0;; ++k) {
     const bool have_cur = cur < p.ntiles;
     const bool have2 = t2 < p.ntiles;  // tile k-2 is copied out this iteration
-    // the workgroup that decoded tile rG + (r mod n_r) leads round r (n_r tiles) one
-    // iteration later: every round, the last partial one included, has a leader
-    const uint32_t lr = t1 < p.ntiles ? t1 / G : NONE;
-    const bool lead = lr != NONE && t1 % G == lr % min(G, p.ntiles - lr * G);
     if (!have_cur && t1 >= p.ntiles && !have2) break;
     if (last_tile_k != NONE && k > last_tile_k + 4) {  // cannot happen; never hang the GPU
       if (tid == 0) atomicOr(p.status, (unsigned)GH_ST_TIMEOUT);
       break;
     }
     const uint32_t par = k & 1u;
-    // The second workgroup dispatched to a CU loses every issue-arbitration tie to the
-    // first (age order): alternate the two slots' priority by iteration (cfg4 0.747 ->
-    // 0.729 ms).
-    if (((k + (b >= (G >> 1) ? 1u : 0u)) & 1u) != 0u) __builtin_amdgcn_s_setprio(1);
-    else __builtin_amdgcn_s_setprio(0);
-    // prefix of tile k-2 (R[round] + plocal[tile], lane 0 of every wave) and the
-    // leader's R[lr] and aggregates: loaded mid-decode (a load issued at the top often saw
-    // the value a little before it was published, and the re-poll then paid a full
-    // memory round trip)
-    unsigned long long gr = 0, gp = 0, rl = 0;
-    if (lead && tid == 0 && lr > 0) rl = __hip_atomic_load(&p.rprefix[lr], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t lt = lr * G + (uint32_t)tid * LPL;  // leader: first tile of this lane
-    const uint32_t lend = min(p.ntiles, (lr + 1) * G);
-    bool lvalid[LPL];
-    unsigned long long la[LPL];
-#pragma unroll
-    for (int j = 0; j < LPL; ++j) {
-      lvalid[j] = lead && lt + j < lend;
-      la[j] = 0;
-    }
+    if (ahead) __builtin_amdgcn_s_setprio(0);
+    else __builtin_amdgcn_s_setprio(2);
+    // prefix of tile k-2 (lane 0 of every wave): loaded mid-decode (a load issued at the
+    // top often saw the value a little before it was published, and the re-poll then
+    // paid a full memory round trip)
+    unsigned long long gp = 0;
     auto mid = [&]() {
-      if (have2 && lane == 0) {
-        const uint32_t r2 = t2 / G;
-        gp = __hip_atomic_load(&p.plocal[t2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        gr = r2 == 0 ? 0ull : __hip_atomic_load(&p.rprefix[r2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      if (lead)
-#pragma unroll
-        for (int j = 0; j < LPL; ++j)
-          la[j] = __hip_atomic_load(&p.granules[lvalid[j] ? lt + j : 0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (have2 && lane == 0) gp = __hip_atomic_load(&p.prefix[t2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
     // ---- decode this tile (its words were loaded during the previous iteration) --------
     const uint32_t seg0 = cur * (uint32_t)(U * TB) + (uint32_t)tid;
@@ -384,20 +400,18 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     // ---- copy tile k-2 out (its prefix was published about an iteration ago) ----------
     if (have2) {
       unsigned long long goff = 0;
+      bool polled = false;
       if (lane == 0) {
-        const uint32_t r2 = t2 / G;
-        if (!granule_ok(p, gp, 2)) {
+        polled = !granule_ok(p, gp, 2);
+        if (polled) {
           if (wid == 0) atomicAdd(p.stats, 1ull);
-          gp = poll_granule(p, &p.plocal[t2], 2);
+          gp = poll_granule(p, &p.prefix[t2], 2);
         }
-        if (r2 > 0 && !granule_ok(p, gr, 2)) {
-          if (wid == 0) atomicAdd(p.stats + 1, 1ull);
-          gr = poll_granule(p, &p.rprefix[r2], 2);
-        }
-        goff = (gp & GRAN_VMASK) + (r2 > 0 ? (gr & GRAN_VMASK) : 0ull);
+        goff = gp & GRAN_VMASK;
         if (wid == 0 && t2 == p.ntiles - 1) *p.total = goff + tot2;
       }
       goff = rfl_u64(goff);
+      ahead = __builtin_amdgcn_readfirstlane(polled ? 1 : 0) != 0;
       const uint32_t n2 = goff >= p.out_cap ? 0u : (uint32_t)min<unsigned long long>(tot2, p.out_cap - goff);
       load(nxt);  // the next tile's words, issued before this copy-out's stores
       copy_out_tile<TB, TILE_NS>(p.out, p.lut_bytes + buf * p.stage_bytes, goff, n2, tid,
@@ -412,28 +426,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
       if (lane == 63) s_wsum[(par * U + u) * NWAVE_T + wid] = incl;
       bpos[u] = incl - cnt[u];
     }
-    // leader: every aggregate of the round published?  (rarely not: poll)
-    uint32_t lval[LPL], lsum = 0, lincl = 0;
-    if (lead) {
-      bool ready = true;
-#pragma unroll
-      for (int j = 0; j < LPL; ++j) ready &= !lvalid[j] || granule_ok(p, la[j], 1) || granule_ok(p, la[j], 2);
-      if (!__all(ready)) {
-        if (lane == 0) atomicAdd(p.stats + 2, 1ull);
-#pragma unroll
-        for (int j = 0; j < LPL; ++j)
-          if (lvalid[j] && !(granule_ok(p, la[j], 1) || granule_ok(p, la[j], 2)))
-            la[j] = poll_granule(p, &p.granules[lt + j], 1);
-      }
-#pragma unroll
-      for (int j = 0; j < LPL; ++j) {
-        lval[j] = lvalid[j] ? (uint32_t)(la[j] & GRAN_VMASK) : 0u;  // a tile holds < 2^32 symbols
-        lsum += lval[j];
-      }
-      lincl = wave_incl_scan(lsum);
-      if (lane == 63) s_lead[wid] = lincl;
-    }
-    __syncthreads();  // tile sums, leader batch totals
+    __syncthreads();  // tile sums
     uint32_t tile_total = 0;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -449,31 +442,6 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     tile_total = __builtin_amdgcn_readfirstlane(tile_total);
     if (tid == 0 && have_cur)
       __hip_atomic_store(&p.granules[cur], granule(p.epoch, 1, tile_total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (lead) {  // publish the round's within-round prefixes and R[lr + 1]
-      unsigned long long before = 0, total = 0;
-#pragma unroll
-      for (int q = 0; q < LDR_NB; ++q) {
-        const uint32_t x = s_lead[q];
-        before += (q < wid) ? x : 0u;
-        total += x;
-      }
-      unsigned long long run = before + lincl - lsum;
-#pragma unroll
-      for (int j = 0; j < LPL; ++j) {
-        if (lvalid[j])
-          __hip_atomic_store(&p.plocal[lt + j], granule(p.epoch, 2, run), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        run += lval[j];
-      }
-      if (tid == 0) {
-        if (lr > 0 && !granule_ok(p, rl, 2)) {
-          atomicAdd(p.stats + 3, 1ull);
-          rl = poll_granule(p, &p.rprefix[lr], 2);
-        }
-        const unsigned long long r0 = lr > 0 ? (rl & GRAN_VMASK) : 0ull;
-        __hip_atomic_store(&p.rprefix[lr + 1], granule(p.epoch, 2, r0 + total), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
     if (have_cur) {
       // stage this tile into buffer k & 1 (copied out two iterations later) at its
       // absolute LDS address (the kernel's LDS starts at 0)

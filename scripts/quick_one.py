@@ -15,4 +15,4 @@ for _ in range(reps): d.decode()
 rep = d.report()
 ok = bool(np.array_equal(d.download(s.n), data)) and rep.status == 0
 print(f"{name} ms={rep.kernel_ms:.4f} frac={alg / rep.kernel_ms / 1e6 / 8000:.4f} mode={gh.MODE_NAMES.get(rep.mode)} "
-      f"K={rep.lut_bits} grid={rep.grid} st={rep.status} ok={ok}", flush=True)
+      f"K={rep.lut_bits} grid={rep.grid} st={rep.status} polls={rep.slow_lookbacks / (reps + 3):.0f} ok={ok}", flush=True)
