@@ -34,7 +34,19 @@
 constexpr int TILE_TB = 512;       // threads per workgroup
 constexpr int TILE_U = 2;          // segments per lane
 constexpr int TILE_NS = 2;         // 16-byte stores per thread per copy-out (the rest of a tile loops)
-constexpr int TILE_MIDG = 2;       // decode group after which the mid-decode loads are issued
+#ifndef GH_TILE_MIDG
+#define GH_TILE_MIDG 2
+#endif
+#ifndef GH_TILE_PHI
+#define GH_TILE_PHI 2
+#endif
+#ifndef GH_TILE_PLO
+#define GH_TILE_PLO 0
+#endif
+#ifndef GH_POLL_SLEEP
+#define GH_POLL_SLEEP 2
+#endif
+constexpr int TILE_MIDG = GH_TILE_MIDG;  // decode group after which the mid-decode loads are issued
 constexpr int STAGE_PAD = 16;      // staging byte STAGE_PAD + i = tile byte i
 constexpr int OW = 8;              // output words per segment (32 codewords of >= 4 bits)
 
@@ -261,7 +273,7 @@ __device__ __forceinline__ unsigned long long poll_granule(const TileParams& p, 
         return 0;
       }
     }
-    __builtin_amdgcn_s_sleep(2);
+    __builtin_amdgcn_s_sleep(GH_POLL_SLEEP);
   }
 }
 
@@ -362,8 +374,8 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
       break;
     }
     const uint32_t par = k & 1u;
-    if (ahead) __builtin_amdgcn_s_setprio(0);
-    else __builtin_amdgcn_s_setprio(2);
+    if (ahead) __builtin_amdgcn_s_setprio(GH_TILE_PLO);
+    else __builtin_amdgcn_s_setprio(GH_TILE_PHI);
     // prefix of tile k-2 (lane 0 of every wave): loaded mid-decode (a load issued at the
     // top often saw the value a little before it was published, and the re-poll then
     // paid a full memory round trip)
