@@ -439,19 +439,14 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
       bpos[u] = incl - cnt[u];
     }
     __syncthreads();  // tile sums
-    uint32_t tile_total = 0;
+    // the U x NWAVE_T wave sums in chain-then-wave order, one per lane, scanned with DPP:
+    // wave w's chain-u segments start at the exclusive prefix of entry u * NWAVE_T + w
+    static_assert(U * NWAVE_T <= 64, "one wave sum per lane");
+    const uint32_t xs = lane < U * NWAVE_T ? s_wsum[par * U * NWAVE_T + lane] : 0u;
+    const uint32_t xi = wave_incl_scan(xs);
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      uint32_t add = tile_total;
-#pragma unroll
-      for (int q = 0; q < NWAVE_T; ++q) {
-        const uint32_t x = s_wsum[(par * U + u) * NWAVE_T + q];
-        add += (q < wid) ? x : 0u;
-        tile_total += x;
-      }
-      bpos[u] += add;
-    }
-    tile_total = __builtin_amdgcn_readfirstlane(tile_total);
+    for (int u = 0; u < U; ++u) bpos[u] += (uint32_t)__builtin_amdgcn_readlane((int)(xi - xs), u * NWAVE_T + wid);
+    const uint32_t tile_total = (uint32_t)__builtin_amdgcn_readlane((int)xi, U * NWAVE_T - 1);
     if (tid == 0 && have_cur)
       __hip_atomic_store(&p.granules[cur], granule(p.epoch, 1, tile_total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (have_cur) {

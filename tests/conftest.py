@@ -17,6 +17,13 @@ def pytest_configure(config):
 
 @pytest.fixture(scope="session")
 def gh():
+    # torch first: its wheel bundles its own HIP runtime, and the process must end up with
+    # one (libgaphuff then binds to the already-loaded libamdhip64; loaded the other way
+    # round, torch's later HIP init reports no GPU)
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     import gaphuff
     gaphuff.lib()
     return gaphuff
