@@ -164,7 +164,13 @@ static int tile_setup(gh_ctx* c, uint32_t K) {
   c->tile_k = K;
   c->tile_g = std::min<uint32_t>(4, 32 / cn.maxlen);
   c->ntiles = (uint32_t)ceil_div(c->nseg, (uint64_t)TILE_U * TILE_TB);
-  c->stage_bytes = (uint32_t)((STAGE_PAD + (uint64_t)TILE_U * TILE_TB * maxsyms + 48 + 127) & ~127ull);
+  // Staging is sized for TILE_SCAP bytes per segment, not the worst case (128 / minlen):
+  // two workgroups per CU then fit three segments per lane.  A tile is the sum of 1536
+  // segments, so it stays near its mean (r = 0.1: 16.5 bytes per segment); a larger one
+  // stores straight from registers (gh_tile_kernel).  GH_TILE_SCAP overrides (tests).
+  uint64_t per_seg = std::min<uint64_t>(maxsyms, TILE_SCAP);
+  if (const char* e = getenv("GH_TILE_SCAP")) per_seg = std::min<uint64_t>(maxsyms, (uint64_t)std::max(1, atoi(e)));
+  c->stage_bytes = (uint32_t)((STAGE_PAD + (uint64_t)TILE_U * TILE_TB * per_seg + 48 + 127) & ~127ull);
   const std::vector<uint32_t> lt = grouped_lut(cn, K);
   const void* kern = tile_kernel_for(c->tile_g);
   const char* envr = getenv("GH_LGR");

@@ -94,15 +94,17 @@ __device__ __forceinline__ uint2 lds_u64_nowait(uint32_t a) {
   asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(a) : "memory");
   return v;
 }
-// One wait for the U independent reads of a lookup step, tied to their results so the
+// One wait for the U (1-4) independent reads of a lookup step, tied to their results so the
 // compiler cannot use them before it.
 template <int U, class T>
 __device__ __forceinline__ void lds_wait(T (&v)[U]) {
-  static_assert(U == 1 || U == 2 || U == 4, "lds_wait: 1, 2 or 4 reads");
+  static_assert(U >= 1 && U <= 4, "lds_wait: 1 to 4 reads");
   if constexpr (U == 1) {
     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0])::"memory");
   } else if constexpr (U == 2) {
     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1])::"memory");
+  } else if constexpr (U == 3) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2])::"memory");
   } else {
     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3])::"memory");
   }

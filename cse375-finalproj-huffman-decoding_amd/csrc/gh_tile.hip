@@ -4,7 +4,7 @@
 // look-back (:571-653) and second decode that writes the bytes (:655-728) — as ONE
 // decode pass per segment in one persistent kernel.
 //
-// 512-thread workgroups, two segments per lane, a tile = 1024 consecutive segments.
+// 512-thread workgroups, three segments per lane, a tile = 1536 consecutive segments.
 // Workgroup 0 is the round leader; the D = grid - 1 others decode: workgroup b takes
 // tiles b, b + D, b + 2D, ... (static round robin; grid <= 512).  Iteration k of a
 // decoding workgroup:
@@ -15,7 +15,9 @@
 //   copy tile k-2 out of staging (its prefix has had an iteration to arrive), with a
 //     fixed store count; the next tile's loads are issued just before
 //   wave scans of the counts -> BARRIER -> publish tile k's aggregate
-//   stage tile k (aligned dword stores, a second barrier, the 1-3 head bytes)
+//   stage tile k (aligned dword stores, a second barrier, the 1-3 head bytes); a tile
+//     larger than staging (20 bytes per segment) waits for its prefix and stores its
+//     bytes straight from registers
 //
 // The leader takes the rounds (tiles rD .. rD + D - 1) in order: it waits for a round's
 // aggregates, scans them and publishes every tile's global exclusive prefix.  The start
@@ -32,8 +34,15 @@
 // 0.68 ms; alternating the two slots' priority by iteration gave 0.747 -> 0.729 ms).
 
 constexpr int TILE_TB = 512;       // threads per workgroup
-constexpr int TILE_U = 2;          // segments per lane
-constexpr int TILE_NS = 2;         // 16-byte stores per thread per copy-out (the rest of a tile loops)
+#ifndef GH_TILE_U
+#define GH_TILE_U 3
+#endif
+#ifndef GH_TILE_NS
+#define GH_TILE_NS 2
+#endif
+constexpr int TILE_U = GH_TILE_U;    // segments per lane
+constexpr int TILE_NS = GH_TILE_NS;  // 16-byte stores per thread per copy-out (the rest of a tile loops)
+constexpr int TILE_SCAP = 20;        // staging bytes per segment (larger tiles bypass staging)
 #ifndef GH_TILE_MIDG
 #define GH_TILE_MIDG 2
 #endif
@@ -245,6 +254,15 @@ __device__ __forceinline__ void copy_out_tile(uint8_t* out, uint32_t stg, unsign
   *((real || hb) ? o + k : (uint8_t*)junk) = (uint8_t)b;
 }
 
+// A segment's n bytes (ow, byte 0 first) stored to out[o, o + n), clamped at cap: the
+// path of a tile too large for staging (byte stores; rare).
+__device__ __forceinline__ void store_direct(uint8_t* out, unsigned long long cap, unsigned long long o,
+                                             const uint32_t (&ow)[OW], uint32_t n) {
+#pragma unroll
+  for (int i = 0; i < 4 * OW; ++i)
+    if ((uint32_t)i < n && o + (uint32_t)i < cap) out[o + (uint32_t)i] = (uint8_t)(ow[i >> 2] >> (8 * (i & 3)));
+}
+
 __device__ __forceinline__ bool granule_ok(const TileParams& p, unsigned long long v, uint32_t flag) {
   return (uint32_t)(v >> 40) == p.epoch && (uint32_t)((v >> 38) & 3u) == flag;
 }
@@ -449,7 +467,22 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     const uint32_t tile_total = (uint32_t)__builtin_amdgcn_readlane((int)xi, U * NWAVE_T - 1);
     if (tid == 0 && have_cur)
       __hip_atomic_store(&p.granules[cur], granule(p.epoch, 1, tile_total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (have_cur) {
+    // staging holds a tile of up to stage_bytes - STAGE_PAD - 48 bytes (sized for the
+    // typical tile, not the worst case: see tile_setup); a larger tile waits for its own
+    // prefix here and stores its bytes straight from registers
+    const bool staged = have_cur && tile_total + (uint32_t)(STAGE_PAD + 48) <= p.stage_bytes;
+    if (have_cur && !staged) {
+      unsigned long long goff = 0;
+      if (lane == 0) {
+        unsigned long long g = __hip_atomic_load(&p.prefix[cur], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!granule_ok(p, g, 2)) g = poll_granule(p, &p.prefix[cur], 2);
+        goff = g & GRAN_VMASK;
+        if (wid == 0 && cur == p.ntiles - 1) *p.total = goff + tile_total;
+      }
+      goff = rfl_u64(goff);
+#pragma unroll
+      for (int u = 0; u < U; ++u) store_direct(p.out, p.out_cap, goff + bpos[u], ow[u], cnt[u]);
+    } else if (have_cur) {
       // stage this tile into buffer k & 1 (copied out two iterations later) at its
       // absolute LDS address (the kernel's LDS starts at 0)
       const uint32_t sbase = p.lut_bytes + buf * p.stage_bytes + STAGE_PAD;
@@ -468,7 +501,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     }
     t2 = t1;
     tot2 = tot1;
-    t1 = have_cur ? cur : NONE;
+    t1 = staged ? cur : NONE;
     tot1 = tile_total;
     buf ^= 1u;
     cur = nxt < p.ntiles ? nxt : NONE;

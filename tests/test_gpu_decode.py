@@ -329,14 +329,18 @@ def test_wave_split_count_lut_widths(gpu, orc, kc, monkeypatch):
             assert rep.symbols == sum(orc.segment_count(img, i) for i in range(s.g))
 
 
-@pytest.mark.parametrize("mode,r", [("wsplit", 0.5), ("wsplit", 0.9), ("tile", 0.1)])
-def test_output_capacity_below_total(gpu, mode, r, monkeypatch):
+@pytest.mark.parametrize("mode,r,scap", [("wsplit", 0.5, None), ("wsplit", 0.9, None), ("tile", 0.1, None),
+                                         ("tile", 0.1, "4")])
+def test_output_capacity_below_total(gpu, mode, r, scap, monkeypatch):
     """An output capacity below the stream's total (gh_ctx_load out_cap) writes exactly
     the prefix that fits: caps inside the first chunk, mid-range, at a range edge and
     just below the end, on the default grid and (wave split) on 3 workgroups, whose
     long ranges are staged in many pieces (a piece that crosses the cap must not be
-    followed by writes of later pieces)."""
+    followed by writes of later pieces).  scap: tile staging for 4 bytes per segment,
+    so every tile takes the direct-store path."""
     monkeypatch.setenv("GH_MODE", mode)
+    if scap:
+        monkeypatch.setenv("GH_TILE_SCAP", scap)
     data = gpu.generate(81, r, 2_000_003)
     s = gpu.parse(gpu.encode(data))
     for grid in (("", "3") if mode == "wsplit" else ("",)):
@@ -352,6 +356,31 @@ def test_output_capacity_below_total(gpu, mode, r, monkeypatch):
                 if not np.array_equal(got, data[:cap]):
                     bad = np.nonzero(got != data[:cap])[0]
                     raise AssertionError(f"{mode} grid={grid} cap={cap}: {bad.size} wrong bytes, first at {bad[0]}")
+
+
+@pytest.mark.parametrize("scap", [None, "17", "4"])
+def test_tile_staging_overflow(gpu, orc, scap, monkeypatch):
+    """The tile kernel's staging holds 20 bytes per segment (the typical tile, not the
+    worst case 128 / minlen); a tile decoding to more bytes waits for its own prefix and
+    stores straight from registers.  Data sorted by falling symbol frequency puts the
+    shortest codewords first, so its first tiles overflow (25.6 symbols per segment on
+    5-bit codewords); staging caps of 17 and 4 bytes per segment send about half / all
+    of a random stream's tiles through the direct path."""
+    monkeypatch.setenv("GH_MODE", "tile")
+    if scap:
+        monkeypatch.setenv("GH_TILE_SCAP", scap)
+    d = gpu.generate(31, 0.1, 3_000_001)
+    vals, cnts = np.unique(d, return_counts=True)
+    rank = np.zeros(256, np.int64)
+    rank[vals[np.argsort(-cnts, kind="stable")]] = np.arange(vals.size)
+    dense = d[np.argsort(rank[d], kind="stable")]
+    for x in (dense, d):
+        img = _roundtrip(gpu, orc, x)
+        with gpu.Decoder(0) as dec:
+            dec.load(gpu.parse(img))
+            dec.decode()
+            rep = dec.report()
+        assert gpu.MODE_NAMES[rep.mode] == "tile" and rep.status == 0
 
 
 @pytest.mark.parametrize("mode", ["tile", "wsplit"])
