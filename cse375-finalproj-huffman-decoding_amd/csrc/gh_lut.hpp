@@ -3,7 +3,7 @@
 // one fixed 10-bit single-symbol table (decoder/src/get_table.cpp:15-95) that is wrong
 // for maxlen < 10; these tables are sized by the code itself.
 //
-//   tile kernel (grouped codes)  u32 {len | sym << 24}, one codeword per lookup;
+//   tile kernel (grouped codes)  u32 {len | sym << 8 | len << 23}, one codeword per lookup;
 //   wave split, count pass       u32 {b | end mask << 16}: every codeword wholly inside
 //                                the Kc-bit window (bit e-1 of the mask per codeword
 //                                end e, b = their bits);
@@ -74,14 +74,14 @@ inline bool grouped_code(const Canon& c) {
   return c.nsyms > 0 && c.minlen >= 4 && c.maxlen <= 12 && kraft16(c) == 65536 && multi_gain(c, 12) < 1.5;
 }
 
-// Tile kernel LUT of width K >= maxlen: entry i = {len | sym << 24} of the codeword at
-// the top of i.
+// Tile kernel LUT of width K >= maxlen: entry i = {len | sym << 8 | len << 23} of the
+// codeword at the top of i (the layout of the tile kernel's decode state, gh_tile.hip).
 inline std::vector<uint32_t> grouped_lut(const Canon& c, uint32_t K) {
   std::vector<uint32_t> t(std::max<uint32_t>(1u << K, 4), 0u);
   for (uint32_t i = 0; i < (1u << K); ++i) {
     uint32_t fi = 0;
     const uint32_t l = canon_decode16(c, (i << (32 - K)) >> 16, &fi);
-    t[i] = l | ((uint32_t)c.sym[fi] << 24);
+    t[i] = l | ((uint32_t)c.sym[fi] << 8) | (l << 23);
   }
   return t;
 }

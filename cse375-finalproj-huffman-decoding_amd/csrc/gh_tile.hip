@@ -62,7 +62,7 @@ constexpr int OW = 8;              // output words per segment (32 codewords of 
 struct TileParams {
   const uint32_t* payload;       // local segment j owns words [4j, 4j+4); +1 look-ahead, zero padded
   const uint32_t* gaps;          // gap words; nibble (gap_nib0 + j - 1) = start of local segment j>=1
-  const uint32_t* lut;           // 2^K u32 {len | sym << 24}
+  const uint32_t* lut;           // 2^K u32 {len | sym << 8 | len << 23}
   uint8_t* out;
   unsigned long long* granules;  // one per tile: its symbol count (flag 1)
   unsigned long long* prefix;    // one per tile: its global exclusive prefix (flag 2, by the leader)
@@ -82,9 +82,9 @@ inline size_t tile_lds_bytes(size_t lut_bytes, size_t stage_bytes) {
   return lut_bytes + 2 * stage_bytes + 2 * (TILE_TB / 64) * 4 * TILE_U + 4 * (TILE_TB / 64) + 32;
 }
 
-// v_perm selector placing byte 3 of S0 (the symbol) at byte j, keeping S1's others.
+// v_perm selector placing byte 1 of S0 (the symbol) at byte j, keeping S1's others.
 __device__ __forceinline__ constexpr uint32_t perm_sel(int j) {
-  return j == 0 ? 0x03020107u : j == 1 ? 0x03020700u : j == 2 ? 0x03070100u : 0x07020100u;
+  return j == 0 ? 0x03020105u : j == 1 ? 0x03020500u : j == 2 ? 0x03050100u : 0x05020100u;
 }
 
 // e-window of a segment starting at bit `start` (0..15): e-stream bit 0 is segment
@@ -100,15 +100,29 @@ __device__ __forceinline__ void make_ewin(uint4 w, uint32_t w4, int start, uint3
   e[4] = __builtin_amdgcn_alignbit(w.w, w4, r);
 }
 
+// Decode state of a segment, one register Q:
+//   bits 0-7    32 - bits consumed in the current group (v_alignbit reads bits 0-4);
+//   bits 8-22   symbol underflow room (the entries' symbol bytes are subtracted here);
+//   bits 23-31  H = bits left before the segment end, minus 1 (9 bits).
+// LUT entries are {len | sym << 8 | len << 23}, so Q -= entry advances both counters in
+// one op, and its borrow is set exactly when H < len: at the codeword that reaches or
+// crosses the segment end, the last one the reference keeps (it keeps a codeword iff it
+// starts before the end).  The count is then the index of that codeword + 1 (one
+// v_cndmask on the borrow).  Past it H has wrapped to >= 500 and stays above 127 (at most
+// 32 x 12 more bits are subtracted), so no later codeword borrows; an inactive segment
+// starts at H = 511.
+constexpr uint32_t Q_SYMROOM = 0x7FFFu << 8;
+constexpr uint32_t Q_LIVE = 128u << 23;  // Q below this: the next codeword is still kept
+__device__ __forceinline__ uint32_t q_init(bool act, int start) {
+  return ((act ? (uint32_t)(127 - start) : 511u) << 23) | Q_SYMROOM | 32u;
+}
+
 // Decode of U segments per lane on e-windows, the U chains in lock-step (their LDS
 // reads are independent, so their latencies overlap).  Each group decodes G codewords
-// per chain from e0:e1 and then shifts the windows.  q counts down from 32 by whole LUT
-// entries {len | sym << 24}: its low 24 bits stay exact, v_alignbit reads only the low
-// 5, and the liveness test q > T (the codeword starts before the segment end; T = F +
-// 32 - L, F = bits flushed so far, L = 128 - start) reads the low 16 sign-extended
-// (SDWA).  Codeword j of a segment goes to byte j of ow (v_perm, static index); dead
-// codewords go there too and are never staged.  `mid()` runs once, after group MIDG
-// (or at the end if the loop stops earlier).
+// per chain from e0:e1 and then shifts the windows (G * maxlen <= 32, so the group's
+// consumed bits fit Q's low byte).  Codeword j of a segment goes to byte j of ow (v_perm,
+// static index); dead codewords go there too and are never staged.  `mid()` runs once,
+// after group MIDG (or at the end if the loop stops earlier).
 template <int G, int U, int MIDG, class Mid>
 __device__ __forceinline__ void decode_tile_grouped(uint32_t (&e)[U][5], const int (&start)[U],
                                                     const bool (&act)[U], uint32_t (&ow)[U][OW],
@@ -117,11 +131,9 @@ __device__ __forceinline__ void decode_tile_grouped(uint32_t (&e)[U][5], const i
   constexpr int S = 4 * OW;
   constexpr int NG = (S + G - 1) / G;
   uint32_t q[U];
-  int T[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    q[u] = 32;
-    T[u] = act[u] ? start[u] - 96 : 0x3FFFFFFF;  // inactive: never live, no overflow
+    q[u] = q_init(act[u], start[u]);
     cnt[u] = 0;
 #pragma unroll
     for (int k = 0; k < OW; ++k) ow[u][k] = 0;
@@ -142,15 +154,14 @@ __device__ __forceinline__ void decode_tile_grouped(uint32_t (&e)[U][5], const i
         lds_wait(ent);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          asm("v_cmp_gt_i32_sdwa vcc, sext(%1), %2 src0_sel:WORD_0 src1_sel:DWORD\n\t"
-              "v_addc_co_u32 %0, vcc, 0, %0, vcc"
-              : "+v"(cnt[u]) : "v"(q[u]), "v"(T[u]) : "vcc");
+          asm("v_sub_co_u32 %0, vcc, %0, %2\n\t"
+              "v_cndmask_b32_e64 %1, %1, %3, vcc"
+              : "+v"(q[u]), "+v"(cnt[u]) : "v"(ent[u]), "i"(pos + 1) : "vcc");
           ow[u][pos >> 2] = __builtin_amdgcn_perm(ent[u], ow[u][pos >> 2], perm_sel(pos & 3));
-          q[u] -= ent[u];
         }
       }
     }
-    bool more = false;
+    uint32_t qmin = 0xFFFFFFFFu;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       e[u][0] = __builtin_amdgcn_alignbit(e[u][0], e[u][1], q[u]);
@@ -158,15 +169,14 @@ __device__ __forceinline__ void decode_tile_grouped(uint32_t (&e)[U][5], const i
       e[u][2] = __builtin_amdgcn_alignbit(e[u][2], e[u][3], q[u]);
       e[u][3] = __builtin_amdgcn_alignbit(e[u][3], e[u][4], q[u]);
       e[u][4] = __builtin_amdgcn_alignbit(e[u][4], 0u, q[u]);
-      T[u] += 32 - (int)(int16_t)q[u];
-      q[u] = 32;
-      more |= 32 > T[u];
+      q[u] = (q[u] & 0xFFFFFF00u) | 32u;
+      qmin = min(qmin, q[u]);
     }
     if (gi == MIDG) {
       mid();
       mid_done = true;
     }
-    if (gi + 1 < NG && !__any(more)) break;
+    if (gi + 1 < NG && !__any(qmin < Q_LIVE)) break;
   }
   if (!mid_done) mid();
 }
