@@ -191,10 +191,10 @@ static int tile_setup(gh_ctx* c, uint32_t K) {
   c->lgr = (uint32_t)best_lg;
   c->lut_bytes = 4ull << (K + best_lg);
   c->lds = tile_lds_bytes(c->lut_bytes, c->stage_bytes);
-  // workgroup 0 leads the rounds (one aggregate per thread: D = grid - 1 < TILE_TB), the
+  // workgroup 0 leads the rounds (up to LEAD_A aggregates per thread: D = grid - 1 < LEAD_A * TILE_TB), the
   // others decode; every workgroup must be resident at once (the grid is sized from the
   // occupancy; decodes on one device are chained, see DevChain)
-  c->grid = (uint32_t)std::min<uint64_t>({(uint64_t)c->ntiles + 1, (uint64_t)best * c->num_cu, (uint64_t)TILE_TB});
+  c->grid = (uint32_t)std::min<uint64_t>({(uint64_t)c->ntiles + 1, (uint64_t)best * c->num_cu, (uint64_t)LEAD_A * TILE_TB});
   if (c->grid < 2) return GH_OK;  // (the wave split then takes the code)
   GH_HIP(hipMalloc(&c->d_tile_junk, 16ull * c->grid * TILE_TB));
   c->tile = true;

@@ -6,7 +6,7 @@
 //
 // 512-thread workgroups, three segments per lane, a tile = 1536 consecutive segments.
 // Workgroup 0 is the round leader; the D = grid - 1 others decode: workgroup b takes
-// tiles b, b + D, b + 2D, ... (static round robin; grid <= 512).  Iteration k of a
+// tiles b, b + D, b + 2D, ... (static round robin; grid <= 2048).  Iteration k of a
 // decoding workgroup:
 //
 //   decode tile k into registers (one codeword per lookup, G codewords per window shift;
@@ -39,6 +39,9 @@ constexpr int TILE_TB = 512;       // threads per workgroup
 #endif
 #ifndef GH_TILE_NS
 #define GH_TILE_NS 2
+#endif
+#ifndef GH_TILE_WPE
+#define GH_TILE_WPE 4  // waves per SIMD the kernel is compiled for (2 workgroups per CU: 128 VGPRs)
 #endif
 constexpr int TILE_U = GH_TILE_U;    // segments per lane
 constexpr int TILE_NS = GH_TILE_NS;  // 16-byte stores per thread per copy-out (the rest of a tile loops)
@@ -306,26 +309,35 @@ __device__ __forceinline__ unsigned long long poll_granule(const TileParams& p, 
 }
 
 // The round leader (workgroup 0): for every round r of D = grid - 1 tiles, wait for the
-// round's aggregates (one per thread), scan them and publish each tile's global
-// exclusive prefix; R, the start of the round, stays in a register.  (Spreading the
-// rounds over the leader's waves, eight rounds' loads in flight, measured slower.)
+// round's aggregates (thread t takes the A = ceil(D / TB) <= LEAD_A consecutive tiles
+// t*A .. t*A + A - 1 of the round), scan them and publish each tile's global exclusive
+// prefix; R, the start of the round, stays in a register.  (Spreading the rounds over the
+// leader's waves, eight rounds' loads in flight, measured slower.)
+constexpr int LEAD_A = 4;
 template <int TB>
 __device__ __forceinline__ void tile_round_leader(const TileParams& p, uint32_t* s_lead, int tid, int lane, int wid) {
   const uint32_t D = gridDim.x - 1;
+  const uint32_t A = (D + TB - 1) / TB;  // <= LEAD_A (the host caps the grid)
   const uint32_t nr = (p.ntiles + D - 1) / D;
   unsigned long long R = 0;
   for (uint32_t r = 0; r < nr; ++r) {
     const uint32_t t0 = r * D, n = min(D, p.ntiles - t0);
-    uint32_t v = 0;
-    if ((uint32_t)tid < n) {
-      unsigned long long g = __hip_atomic_load(&p.granules[t0 + tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (!granule_ok(p, g, 1)) {
-        atomicAdd(p.stats + 1, 1ull);
-        g = poll_granule(p, &p.granules[t0 + tid], 1);
+    uint32_t v[LEAD_A], sum = 0;
+#pragma unroll
+    for (int i = 0; i < LEAD_A; ++i) {
+      const uint32_t j = (uint32_t)tid * A + (uint32_t)i;
+      v[i] = 0;
+      if ((uint32_t)i < A && j < n) {
+        unsigned long long g = __hip_atomic_load(&p.granules[t0 + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!granule_ok(p, g, 1)) {
+          atomicAdd(p.stats + 1, 1ull);
+          g = poll_granule(p, &p.granules[t0 + j], 1);
+        }
+        v[i] = (uint32_t)(g & GRAN_VMASK);  // a tile holds < 2^32 symbols
       }
-      v = (uint32_t)(g & GRAN_VMASK);  // a tile holds < 2^32 symbols
+      sum += v[i];
     }
-    const uint32_t incl = wave_incl_scan(v);
+    const uint32_t incl = wave_incl_scan(sum);
     if (lane == 63) s_lead[wid] = incl;
     __syncthreads();
     unsigned long long before = 0, total = 0;
@@ -335,9 +347,14 @@ __device__ __forceinline__ void tile_round_leader(const TileParams& p, uint32_t*
       before += (q < wid) ? x : 0u;
       total += x;
     }
-    if ((uint32_t)tid < n)
-      __hip_atomic_store(&p.prefix[t0 + tid], granule(p.epoch, 2, R + before + incl - v), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long run = R + before + incl - sum;
+#pragma unroll
+    for (int i = 0; i < LEAD_A; ++i) {
+      const uint32_t j = (uint32_t)tid * A + (uint32_t)i;
+      if ((uint32_t)i < A && j < n)
+        __hip_atomic_store(&p.prefix[t0 + j], granule(p.epoch, 2, run), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      run += v[i];
+    }
     R += total;
     __syncthreads();
   }
@@ -346,7 +363,7 @@ __device__ __forceinline__ void tile_round_leader(const TileParams& p, uint32_t*
 // TB threads, U segments per lane, GRP codewords per window shift.  Compiled for at most
 // 4 waves per SIMD (two workgroups per CU: 128 VGPRs).
 template <int TB, int U, int GRP>
-__global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void gh_tile_kernel(const TileParams p) {
+__global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE, GH_TILE_WPE))) void gh_tile_kernel(const TileParams p) {
   constexpr int NWAVE_T = TB / 64;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* s_stage = smem + p.lut_bytes;                        // 2 buffers
