@@ -31,6 +31,23 @@ __device__ __forceinline__ Win make_win(uint4 w, uint32_t w4, int s) {
   return v;
 }
 
+// The window pre-shifted right by S bits (the "e-window", 16 <= S <= 31, start <= 15):
+// bits before the segment read as 0, and the K-bit index of the codeword at the window
+// position sits at bits [31 - S - K + 1, 31 - S], so with S = 32 - K - log2(entry bytes)
+// a lookup address is x & mask: one op fewer than (x >> sh) & mask.  It holds the
+// segment's bits up to 160 - S past its start; a codeword that starts before bit 128 and
+// is at most K bits long ends inside it.
+__device__ __forceinline__ Win make_ewin(uint4 w, uint32_t w4, int start, uint32_t S) {
+  const uint32_t r = S - (uint32_t)start;  // 1..31
+  Win v;
+  v.d0 = __builtin_amdgcn_alignbit(0u, w.x, r);
+  v.d1 = __builtin_amdgcn_alignbit(w.x, w.y, r);
+  v.d2 = __builtin_amdgcn_alignbit(w.y, w.z, r);
+  v.d3 = __builtin_amdgcn_alignbit(w.z, w.w, r);
+  v.d4 = __builtin_amdgcn_alignbit(w.w, w4, r);
+  return v;
+}
+
 // Advance the window by 32 - (q & 31) bits (v_alignbit reads the low 5 bits of q).
 __device__ __forceinline__ void win_shift(Win& v, uint32_t q) {
   v.d0 = __builtin_amdgcn_alignbit(v.d0, v.d1, q);

@@ -171,7 +171,7 @@ __global__ __launch_bounds__(TBK) void gh_ws_count_kernel(const WsParams p) {
   static_assert(!FB || GL <= 2, "fallback lookups take up to 16 bits: two per window shift");
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int tid = threadIdx.x, lane = tid & 63;
-  const uint32_t sh = 30u - p.kbits;  // index bits -> byte offset of a u32 entry
+  const uint32_t sh = 30u - p.kbits;  // index bits -> byte offset of a u32 entry (the e-window's S without FB)
   const uint32_t amask = ((1u << p.kbits) - 1u) << 2;
   uint32_t* s_fb = (uint32_t*)(smem + p.lut_bytes);
   uint32_t bad = 0;
@@ -201,7 +201,7 @@ __global__ __launch_bounds__(TBK) void gh_ws_count_kernel(const WsParams p) {
         const int start = seg == 0 ? (int)p.first_start : (int)gap_nib(ga[u], p.gap_nib0 + seg - 1u);
         const int E = (p.last_end && seg == p.nseg - 1u) ? (int)p.last_end
                                                          : 128 + (int)gap_nib(gb[u], p.gap_nib0 + seg);
-        v[u] = make_win(w[u], w4[u], start);
+        v[u] = FB ? make_win(w[u], w4[u], start) : make_ewin(w[u], w4[u], start, sh);
         R[u] = act[u] ? E - start : 0;
         cnt[u] = 0;
       }
@@ -220,7 +220,7 @@ __global__ __launch_bounds__(TBK) void gh_ws_count_kernel(const WsParams p) {
           for (int u = 0; u < U; ++u) {
             const uint32_t x = j == 0 ? v[u].d0 : __builtin_amdgcn_alignbit(v[u].d0, v[u].d1, q[u]);
             xs[u] = x;
-            asm volatile("ds_read_b32 %0, %1" : "=v"(e[u]) : "v"((x >> sh) & amask) : "memory");
+            asm volatile("ds_read_b32 %0, %1" : "=v"(e[u]) : "v"(FB ? (x >> sh) & amask : x & amask) : "memory");
           }
           lds_wait(e);
   #pragma unroll
@@ -329,7 +329,7 @@ __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
   constexpr int NWAVE = TBK / 64;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const uint32_t sh = 29u - p.kbits;
+  const uint32_t sh = 29u - p.kbits;  // index bits -> byte offset of a u64 entry (the e-window's S without FB)
   const uint32_t amask = ((1u << p.kbits) - 1u) << 3;
   uint32_t* s_fb = (uint32_t*)(smem + p.lut_bytes + (uint32_t)NWAVE * p.stage_bytes);
   uint32_t bad = 0;
@@ -415,7 +415,7 @@ __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const bool on = nh == 1 || (uint32_t)u == h;
-          v[u] = make_win(wc[u], w4c[u], start[u]);
+          v[u] = FB ? make_win(wc[u], w4c[u], start[u]) : make_ewin(wc[u], w4c[u], start[u], sh);
           // a chain not staged in this piece: an empty range inside the staging
           ptr[u] = on ? stage0 + 16u + lb + (nh == 1 ? coff[u] : 0u) + bpos[u] : stage0 + 4u * (uint32_t)lane;
           end[u] = on ? ptr[u] + cc[u] : ptr[u];
@@ -432,7 +432,7 @@ __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
             for (int u = 0; u < U; ++u) {
               const uint32_t x = j == 0 ? v[u].d0 : __builtin_amdgcn_alignbit(v[u].d0, v[u].d1, q[u]);
               xs[u] = x;
-              e[u] = lds_u64_nowait((x >> sh) & amask);
+              e[u] = lds_u64_nowait(FB ? (x >> sh) & amask : x & amask);
             }
             lds_wait(e);
 #pragma unroll
