@@ -25,7 +25,7 @@ def _check(gh, orc, data, force_version=0):
 
 
 @pytest.mark.parametrize("r", [0.0, 0.1, 0.5, 0.9, 0.999, 1.0])
-@pytest.mark.parametrize("n", [1, 2, 15, 16, 17, 4095, 4096, 4097, 65549, 1_000_003])
+@pytest.mark.parametrize("n", [1, 2, 15, 16, 17, 1023, 1024, 1025, 2049, 4095, 4096, 4097, 65549, 1_000_003])
 def test_generated_vs_oracle(gpu, orc, r, n):
     _check(gpu, orc, gpu.generate(2000 + n, r, n))
 
