@@ -136,11 +136,19 @@ __device__ __forceinline__ void ws_lut_to_lds(const WsParams& p, uint8_t* smem, 
 // Used where a LUT entry holds no codeword (the first one is longer than the table
 // width, or the pattern is outside an incomplete code: then `bad`, and the longest
 // length, which keeps the count and the write in step).
-// allowed-ends mask for R bits left: bit e-1 set for ends e <= R, all ones if R >= 32,
-// none once the segment is finished (R <= 0; 1-bit codewords end at offset 1).
+// allowed-ends mask for R bits left: bit e-1 set for ends e <= R; none once the segment
+// is finished (R <= 0).  Without the fallback a lookup group ends its codewords at most
+// GL * Kc <= 31 bits past its start, so R is clamped at 31 (v_med3 + v_bfm); with it
+// (two lookups of up to 16 bits) ends reach bit 32: all ones for R >= 32.
+template <bool FB>
 __device__ __forceinline__ uint32_t ws_rmask(int R) {
-  const uint32_t m = 0xFFFFFFFFu >> (32u - (uint32_t)min(max(R, 1), 32));
-  return R > 0 ? m : 0u;
+  if constexpr (FB) {
+    const uint32_t m = 0xFFFFFFFFu >> (32u - (uint32_t)min(max(R, 1), 32));
+    return R > 0 ? m : 0u;
+  } else {
+    const uint32_t r = (uint32_t)min(max(R, 0), 31);
+    return (1u << r) - 1u;
+  }
 }
 
 __device__ __forceinline__ uint32_t ws_canon(const uint32_t* s_fb, uint32_t w16, uint32_t lo, uint32_t hi,
@@ -162,7 +170,7 @@ __device__ __forceinline__ void ws_fb_to_lds(const WsParams& p, uint32_t* s_fb, 
 // of them, no cap), end-mask bit e-1 per codeword end e.  One lookup step:
 //   cnt += popcount(endmask & rm)   (SDWA AND of the high half, v_bcnt)
 //   rm >>= b                        (v_ashrrev reads only the low 5 bits of the entry)
-//   q -= entry                      (q's low 16 bits stay exact: sum of b <= 32)
+//   q -= b                          (SDWA low half: q = -bits consumed in the group)
 // FB: codes longer than Kc or incomplete codes; an entry with no codeword (b = 0) is
 // replaced by the canonical codeword's {len, end mask 1 << (len-1)} (GL = 2 then: two
 // lookups of up to 16 bits fit one 32-bit window shift).
@@ -210,8 +218,8 @@ __global__ __launch_bounds__(TBK) void gh_ws_count_kernel(const WsParams p) {
         uint32_t rm[U], q[U];
   #pragma unroll
         for (int u = 0; u < U; ++u) {
-          rm[u] = ws_rmask(R[u]);
-          q[u] = 32u;
+          rm[u] = ws_rmask<FB>(R[u]);
+          q[u] = 0u;
         }
   #pragma unroll
         for (int j = 0; j < GL; ++j) {
@@ -236,14 +244,15 @@ __global__ __launch_bounds__(TBK) void gh_ws_count_kernel(const WsParams p) {
                 : "=v"(m) : "v"(e[u]), "v"(rm[u]));
             cnt[u] = __builtin_popcount(m) + cnt[u];
             asm("v_ashrrev_i32 %0, %1, %0" : "+v"(rm[u]) : "v"(e[u]));
-            q[u] -= e[u];
+            asm("v_sub_u32_sdwa %0, %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0"
+                : "+v"(q[u]) : "v"(e[u]));
           }
         }
         bool more = false;
   #pragma unroll
         for (int u = 0; u < U; ++u) {
-          win_shift(v[u], q[u]);  // consumed = 32 - (q & 0xFFFF), 2..32: v_alignbit reads q & 31
-          R[u] -= 32 - (int)(q[u] & 0xFFFFu);
+          win_shift(v[u], q[u]);  // q = -consumed (1..31 bits): v_alignbit reads q & 31 = 32 - consumed
+          R[u] += (int)q[u];
           more |= R[u] > 0;
         }
         if (!__any(more)) break;
