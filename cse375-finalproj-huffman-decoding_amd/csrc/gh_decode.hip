@@ -203,9 +203,9 @@ static int tile_setup(gh_ctx* c, uint32_t K) {
 
 // ---- wave split setup ------------------------------------------------------------
 // Count-LUT width Kc in [max(maxlen, 2), 13] maximising bits per VALU op of a lookup
-// group: GL lookups of ~7 ops each plus ~11 ops of window shift and mask upkeep per
-// chain (r=0.9: Kc=13, 11.2 vs 9.4 bits per lookup at 11).  Longer codes: the
-// fallback.  GH_WS_KC overrides (tests).
+// group: GL lookups of ~6 ops each plus ~8 ops of window shift and end upkeep per chain
+// (r=0.9: Kc=13, 10.6 vs 8.5 bits per lookup at 11; r=0.5: Kc=12, 10.3 vs 7.1 at 9-10).
+// Longer codes: the fallback.  GH_WS_KC overrides (tests).
 static uint32_t ws_count_bits(const Canon& cn) {
   const uint32_t lo = std::min<uint32_t>(std::max<uint32_t>(cn.maxlen, 2), 13);
   if (const char* e = getenv("GH_WS_KC")) return (uint32_t)std::clamp(atoi(e), (int)lo, 14);
@@ -213,7 +213,7 @@ static uint32_t ws_count_bits(const Canon& cn) {
   double best_eff = -1;
   for (uint32_t kc = lo; kc <= 13; ++kc) {  // 14 (64 KiB) measured no faster
     const int gl = lookups_per_shift(kc);
-    const double eff = gl * count_lut(cn, kc, nullptr) / (7.0 * gl + 11.0);
+    const double eff = gl * count_lut(cn, kc, nullptr) / (6.0 * gl + 8.0);
     if (eff > best_eff * 1.01) {  // prefer the smaller table unless clearly better
       best_eff = eff;
       best = kc;
