@@ -33,6 +33,8 @@
 // priority 0; one that found it published is behind and takes priority 2 (cfg4 0.70 ->
 // 0.68 ms; alternating the two slots' priority by iteration gave 0.747 -> 0.729 ms).
 
+// Build knobs (make variant VFLAGS=-D...; every alternative value is measured in
+// DESIGN.md's tile-kernel section, the defaults are the fastest).
 constexpr int TILE_TB = 512;       // threads per workgroup
 #ifndef GH_TILE_U
 #define GH_TILE_U 3
