@@ -60,6 +60,9 @@ constexpr int TILE_SCAP = 20;        // staging bytes per segment (larger tiles 
 #ifndef GH_POLL_SLEEP
 #define GH_POLL_SLEEP 2
 #endif
+#ifndef GH_TILE_TRIM
+#define GH_TILE_TRIM 1  // stop shifting window words no kept codeword can still read
+#endif
 constexpr int TILE_MIDG = GH_TILE_MIDG;  // decode group after which the mid-decode loads are issued
 constexpr int STAGE_PAD = 16;      // staging byte STAGE_PAD + i = tile byte i
 constexpr int OW = 8;              // output words per segment (32 codewords of >= 4 bits)
@@ -167,13 +170,20 @@ __device__ __forceinline__ void decode_tile_grouped(uint32_t (&e)[U][5], const i
       }
     }
     uint32_t qmin = 0xFFFFFFFFu;
+    // Window word k holds e-positions [C + 32k, +32) after this shift, C = the bits
+    // consumed so far >= (gi + 1) * G * 4 (a grouped code has no codeword below 4 bits).
+    // A kept codeword starts before segment bit 128, e-position 127 - start + S, and its
+    // lookup reads K bits: nothing at e-position >= 157 - lgr - start is read for a kept
+    // codeword, so a word lying wholly at or above 157 is no longer shifted (its stale
+    // bits reach only such positions; dead codewords decode garbage, never counted).
+    const int CMIN = (gi + 1) * G * 4;  // a constant once the loop is unrolled
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       e[u][0] = __builtin_amdgcn_alignbit(e[u][0], e[u][1], q[u]);
-      e[u][1] = __builtin_amdgcn_alignbit(e[u][1], e[u][2], q[u]);
-      e[u][2] = __builtin_amdgcn_alignbit(e[u][2], e[u][3], q[u]);
-      e[u][3] = __builtin_amdgcn_alignbit(e[u][3], e[u][4], q[u]);
-      e[u][4] = __builtin_amdgcn_alignbit(e[u][4], 0u, q[u]);
+      if (!GH_TILE_TRIM || CMIN + 32 < 157) e[u][1] = __builtin_amdgcn_alignbit(e[u][1], e[u][2], q[u]);
+      if (!GH_TILE_TRIM || CMIN + 64 < 157) e[u][2] = __builtin_amdgcn_alignbit(e[u][2], e[u][3], q[u]);
+      if (!GH_TILE_TRIM || CMIN + 96 < 157) e[u][3] = __builtin_amdgcn_alignbit(e[u][3], e[u][4], q[u]);
+      if (!GH_TILE_TRIM || CMIN + 128 < 157) e[u][4] = __builtin_amdgcn_alignbit(e[u][4], 0u, q[u]);
       q[u] = (q[u] & 0xFFFFFF00u) | 32u;
       qmin = min(qmin, q[u]);
     }
@@ -456,6 +466,15 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE,
         mid();
       }
     }
+    // wave scans of the counts, before the copy-out: placed after it, the compiler waited
+    // for every outstanding load and store (vmcnt(0)) in the middle of the scans
+    uint32_t bpos[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t incl = wave_incl_scan(cnt[u]);
+      if (lane == 63) s_wsum[(par * U + u) * NWAVE_T + wid] = incl;
+      bpos[u] = incl - cnt[u];
+    }
     // ---- copy tile k-2 out (its prefix was published about an iteration ago) ----------
     if (have2) {
       unsigned long long goff = 0;
@@ -477,13 +496,6 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE,
                                  p.junk + (unsigned long long)blockIdx.x * TB + tid);
     } else {
       load(nxt);
-    }
-    uint32_t bpos[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t incl = wave_incl_scan(cnt[u]);
-      if (lane == 63) s_wsum[(par * U + u) * NWAVE_T + wid] = incl;
-      bpos[u] = incl - cnt[u];
     }
     __syncthreads();  // tile sums
     // the U x NWAVE_T wave sums in chain-then-wave order, one per lane, scanned with DPP:
