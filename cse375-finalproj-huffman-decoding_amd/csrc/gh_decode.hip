@@ -315,7 +315,7 @@ static int ws_setup(gh_ctx* c, double avg_seg_bytes) {
   }
   c->ws_nranges = c->grid * (uint32_t)NW;  // one contiguous range per wave of the write grid
   c->ntiles = c->ws_nblocks;
-  GH_HIP(hipMalloc(&c->d_seg_cnt, c->nseg + 16));
+  GH_HIP(hipMalloc(&c->d_seg_cnt, c->nseg + WS_CNT_PAD + 16));
   GH_HIP(hipMalloc(&c->d_ws_junk, 16ull * 64 * c->ws_nranges));
   GH_HIP(hipMalloc(&c->d_rng_tot, 8ull * c->ws_nranges + 16));
   GH_HIP(hipMalloc(&c->d_rng_off, 8ull * c->ws_nranges + 16));

@@ -60,6 +60,9 @@ constexpr int TILE_SCAP = 20;        // staging bytes per segment (larger tiles 
 #ifndef GH_POLL_SLEEP
 #define GH_POLL_SLEEP 2
 #endif
+#ifndef GH_TILE_NOZERO
+#define GH_TILE_NOZERO 1  // leave the decode's output words unzeroed (bytes past the count are never kept)
+#endif
 #ifndef GH_TILE_TRIM
 #define GH_TILE_TRIM 1  // stop shifting window words no kept codeword can still read
 #endif
@@ -143,8 +146,14 @@ __device__ __forceinline__ void decode_tile_grouped(uint32_t (&e)[U][5], const i
   for (int u = 0; u < U; ++u) {
     q[u] = q_init(act[u], start[u]);
     cnt[u] = 0;
+    // ow needs no zeroing: byte j is written by codeword j for every j < cnt, and the
+    // bytes past cnt are never kept (staging phase 2 / the copy-out's length cover them);
+    // an empty asm defines the registers without an instruction (24 v_mov per iteration)
 #pragma unroll
-    for (int k = 0; k < OW; ++k) ow[u][k] = 0;
+    for (int k = 0; k < OW; ++k) {
+      if (GH_TILE_NOZERO) asm volatile("" : "=v"(ow[u][k]));
+      else ow[u][k] = 0;
+    }
   }
   bool mid_done = false;
 #pragma unroll

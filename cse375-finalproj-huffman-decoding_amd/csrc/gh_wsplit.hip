@@ -43,6 +43,7 @@ constexpr int WS_U = 2;     // chains per lane of the write kernel (segments per
 #define GH_WS_UC 4
 #endif
 constexpr int WS_UC = GH_WS_UC;  // chains per lane of the count kernel
+static_assert(GH_WS_UC <= 4, "seg_cnt padding (WS_CNT_PAD) covers a last block of at most 4 chains");
 constexpr int WS_SB = 256;  // segments per superblock: ranges are cut at superblock edges
 constexpr int WS_SCAN_TB = 1024;
 #ifndef GH_WS_PRIO
@@ -65,6 +66,8 @@ constexpr int WS_SCAN_TB = 1024;
 #else
 #define WS_PRIO(blk, b, g) do {} while (0)
 #endif
+
+constexpr uint32_t WS_CNT_PAD = 64 * 4;  // seg_cnt entries past nseg (a last block of <= 4 chains)
 
 struct WsParams {
   const uint32_t* payload;         // local segment j owns words [4j, 4j+4); +1 look-ahead, zero padded
@@ -258,9 +261,12 @@ __global__ __launch_bounds__(TBK) void gh_ws_count_kernel(const WsParams p) {
         if (!__any(more)) break;
       }
       const unsigned long long seg0 = (unsigned long long)blk * (64 * U) + lane;
+      // one store per chain, unconditional (segments past the shard's end land in the
+      // allocation's padding): a fixed store count lets the compiler wait for the next
+      // block's loads with vmcnt(U) instead of vmcnt(0) behind these stores
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        if (act[u] && WS_CK(seg0 + 64ull * u < p.nseg, 0x400)) p.seg_cnt[seg0 + 64ull * u] = (uint8_t)cnt[u];
+        if (WS_CK(seg0 + 64ull * u < p.nseg + WS_CNT_PAD, 0x400)) p.seg_cnt[seg0 + 64ull * u] = (uint8_t)cnt[u];
         tot += act[u] ? cnt[u] : 0u;
       }
     }
