@@ -477,13 +477,17 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE,
     }
     // wave scans of the counts, before the copy-out: placed after it, the compiler waited
     // for every outstanding load and store (vmcnt(0)) in the middle of the scans
-    uint32_t bpos[U];
+    // (the U scans are independent: issued together, their DPP steps interleave without
+    // the wait states one scan alone needs; then one exec-masked block for the stores)
+    uint32_t bpos[U], incl[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t incl = wave_incl_scan(cnt[u]);
-      if (lane == 63) s_wsum[(par * U + u) * NWAVE_T + wid] = incl;
-      bpos[u] = incl - cnt[u];
+    for (int u = 0; u < U; ++u) incl[u] = wave_incl_scan(cnt[u]);
+    if (lane == 63) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) s_wsum[(par * U + u) * NWAVE_T + wid] = incl[u];
     }
+#pragma unroll
+    for (int u = 0; u < U; ++u) bpos[u] = incl[u] - cnt[u];
     // ---- copy tile k-2 out (its prefix was published about an iteration ago) ----------
     if (have2) {
       unsigned long long goff = 0;
