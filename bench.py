@@ -11,7 +11,10 @@ the HIP kernels behind ``gh_ctx_decode`` (include/gaphuff.h).  Default ``cfg4`` 
 configs[3]: 10^9 bytes of generate.cpp-distributed data, redundancy 0.1, per GPU
 (compressed payload 1.01 GB: the north star's "1 GB compressed.huff"; it does not fit
 the 256 MiB Infinity Cache, so every decode streams from HBM).  ``--workload
-cfg2|cfg3|cfg5`` selects the others.
+cfg2|cfg3|cfg5`` selects the others.  The same run then times a second workload (``--sub``,
+default ``cfg5``: redundancy 0.5, 1 GB per GPU, so 8 GB over 8 GPUs = configs[4] literally,
+with its own bit-exact check and RCCL gather) and reports it under ``sub``; ``--sub none``
+skips it.
 
 Weak scaling: at N GPUs the global input is N x 10^9 bytes.  Rank 0 generates and
 encodes the global stream ONCE (v2 header when N, W or G >= 2^31) into a file under
@@ -228,13 +231,152 @@ def end_to_end(img: np.ndarray, args, r: float, dev, threads: int) -> dict:
     return res
 
 
+def run_workload(args, name: str, per_gpu: int, r: float, ctx: dict, keep_image: bool) -> dict:
+    """One timed workload: build (or share) the stream, load this rank's shard, W untimed
+    and K timed decodes between barriers, then the correctness checks and the RCCL
+    gather.  Returns the measurements (rank-local values plus max/sum over ranks)."""
+    import torch
+
+    world, rank, dev, dist, use_dist, threads = (ctx[k] for k in ("world", "rank", "dev", "dist", "use_dist",
+                                                                   "threads"))
+    total = per_gpu * world
+    t0 = time.time()
+    dec = gh.Decoder(ctx["local"])
+    res = {"image": None, "share_dir": None}
+    try:
+        if not use_dist:
+            data = gh.generate(args.seed, r, total, threads=threads)
+            img = gh.encode(data, threads=threads)
+            del data
+            s = gh.parse(img)
+            hdr = {"n": s.n, "w": s.w, "g": s.g, "version": s.version, "file_bytes": int(img.size)}
+            b, e = 0, s.g
+            t1 = time.time()
+            dec.load(s)
+            torch.cuda.synchronize()
+            load_ms = (time.time() - t1) * 1e3
+            del s
+            if keep_image:
+                res["image"] = img
+            del img
+        else:
+            port = os.environ.get("MASTER_PORT", "0")
+            # the stream file: about the input size (r >= 0 codes average <= 8.1 bits a byte)
+            share_dir = gh_dist.pick_share_dir(dist, rank, int(total * 1.05) + (1 << 20), args.shm, dev)
+            res["share_dir"] = share_dir
+            path = os.path.join(share_dir, f"gh_bench_{port}_{name}_{per_gpu}_{world}.huff")
+            if rank == 0 and share_dir != args.shm:
+                log(f"[rank 0] {args.shm} lacks room for the stream: using {share_dir}")
+
+            def make_image():
+                d = gh.generate(args.seed, r, total, threads=threads)
+                return gh.encode(d, threads=threads)
+
+            try:
+                hdr = gh_dist.share_stream(dist, rank, path, make_image, dev)
+                b, e = gh_dist.shard_range(hdr["g"], world, rank)
+                t1 = time.time()
+                dec.load_file(path, b, e)
+                torch.cuda.synchronize()
+                load_ms = (time.time() - t1) * 1e3
+                dist.barrier()
+            finally:  # never leave the stream in RAM-backed tmpfs, whatever failed
+                if rank == 0:
+                    for f in (path, path + ".part"):
+                        try:
+                            os.unlink(f)
+                        except OSError:
+                            pass
+        log(f"[rank {rank}] {name}: N={hdr['n']} W={hdr['w']} G={hdr['g']} v{hdr['version']} shard=[{b},{e}) "
+            f"setup {t1 - t0:.1f}s load {load_ms:.1f} ms")
+
+        stream = torch.cuda.current_stream().cuda_stream
+        for _ in range(args.warmup):
+            dec.decode(stream, timed=False)
+        rep0 = dec.report(stream)  # synchronises, checks status of the warmup launches
+        dec.reset_timing()
+
+        def barrier():
+            if dist is not None:
+                dist.barrier()
+
+        barrier()
+        torch.cuda.synchronize()
+        ts = time.perf_counter()
+        for _ in range(args.steps):
+            dec.decode(stream, timed=True)
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - ts
+        barrier()
+        rep = dec.report(stream)
+        shard_bytes = int(rep.out_bytes)
+
+        alg = gh_dist.shard_alg_bytes(hdr["w"], b, e, shard_bytes)
+        kern_ms = float(rep.kernel_ms)
+        mx, sm = gh_dist.reduce_max_sum(dist, [elapsed, kern_ms, float(shard_bytes)], dev)
+
+        # ---- correctness: each shard vs the generator's slice at its output offset
+        off, sizes = gh_dist.exclusive_offsets(dist, shard_bytes, dev)
+        out = torch.empty(max(1, shard_bytes), dtype=torch.uint8, device=dev)
+        dec.copy_output(out.data_ptr(), shard_bytes, 0, stream)
+        torch.cuda.synchronize()
+        ok = (sum(sizes) == hdr["n"]) and gh_dist.verify_slice(out[:shard_bytes].cpu().numpy(), args.seed, r, off,
+                                                               threads=threads)
+        status_ok = rep.status == 0 and rep0.status == 0
+        gather_ms = None
+        gather_ok = None
+        if dist is not None and not args.no_gather:
+            full, gather_ms = gh_dist.gather_to_root(dist, out, shard_bytes, dev)
+            if rank == 0:
+                gather_ok = full is not None and full.numel() == hdr["n"]
+                for k in range(world):  # gathered shard k == generator slice, compared on the GPU
+                    if not gather_ok:
+                        break
+                    lo = sum(sizes[:k])
+                    want = torch.from_numpy(gh.generate(args.seed, r, sizes[k], offset=lo, threads=threads)).to(dev)
+                    gather_ok = bool(torch.equal(full[lo:lo + sizes[k]], want))
+                    del want
+                del full
+            ok = ok and (gather_ok is not False)
+        ok = gh_dist.all_true(dist, bool(ok and status_ok), dev)
+        del out
+        torch.cuda.empty_cache()
+        res.update({"hdr": hdr, "b": b, "e": e, "rep": rep, "alg": alg, "kern_ms": kern_ms,
+                    "max_elapsed": mx[0], "max_kern": mx[1], "sum_bytes": sm[2], "ok": ok,
+                    "gather_ms": gather_ms, "gather_ok": gather_ok, "load_ms": load_ms, "total": total})
+        return res
+    finally:
+        dec.close()
+
+
+def sub_record(args, name: str, res: dict, r: float, desc: str, per_gpu: int) -> dict:
+    """A second workload timed in the same run (rank 0's summary of run_workload)."""
+    kern_ms = res["kern_ms"]
+    achieved = res["alg"] / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
+    rep = res["rep"]
+    return {"workload": name, "description": desc, "bytes_per_gpu": per_gpu, "global_bytes": res["total"],
+            "redundancy": r, "compressed_bytes": res["hdr"]["file_bytes"], "segments": res["hdr"]["g"],
+            "format_version": res["hdr"]["version"],
+            "value": round(res["sum_bytes"] * args.steps / res["max_elapsed"] / 1e9, 3), "unit": "GB/s",
+            "ms_per_step": round(res["max_elapsed"] / args.steps * 1e3, 4),
+            "kernel_ms": round(kern_ms, 4), "max_kernel_ms_over_ranks": round(res["max_kern"], 4),
+            "roofline_frac": round(achieved / HBM_PEAK_GBPS, 4), "alg_bytes_per_launch": res["alg"],
+            "mode": gh.MODE_NAMES.get(int(rep.mode)), "path": gh.PATH_NAMES.get(int(rep.path)),
+            "bitexact": bool(res["ok"]),
+            "gather_ms": None if res["gather_ms"] is None else round(res["gather_ms"], 3),
+            "gather_bitexact": res["gather_ok"], "load_ms": round(res["load_ms"], 2)}
+
+
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="cfg4", choices=sorted(WORKLOADS))
-    ap.add_argument("--size", type=int, default=0, help="bytes per GPU (overrides workload)")
+    ap.add_argument("--sub", default="cfg5", choices=sorted(WORKLOADS) + ["none"],
+                    help="second workload timed in the same run, reported under 'sub' (default cfg5: "
+                         "r=0.5, 1 GB per GPU = configs[4] at 8 GPUs, with its own RCCL gather)")
+    ap.add_argument("--size", type=int, default=0, help="bytes per GPU (overrides workload and sub)")
     ap.add_argument("--seed", type=int, default=375)
     ap.add_argument("--cpu-sample", type=int, default=10**8,
                     help="bytes decoded by the CPU baseline (0 = skip)")
@@ -269,116 +411,21 @@ def main() -> int:
         os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group("nccl", device_id=dev)
     threads = args.threads or gh_dist.host_threads()
+    ctx = {"world": world, "rank": rank, "local": local, "dev": dev, "dist": dist, "use_dist": use_dist,
+           "threads": threads}
 
     per_gpu, r, desc = WORKLOADS[args.workload]
     if args.size:
         per_gpu = args.size
-    total = per_gpu * world
-
-    t0 = time.time()
-    dec = gh.Decoder(local)
-    e2e_img = None  # N=1: the image, kept for the end-to-end timing
-    share_dir = None
-    if not use_dist:
-        data = gh.generate(args.seed, r, total, threads=threads)
-        img = gh.encode(data, threads=threads)
-        del data
-        s = gh.parse(img)
-        hdr = {"n": s.n, "w": s.w, "g": s.g, "version": s.version, "file_bytes": int(img.size)}
-        b, e = 0, s.g
-        t1 = time.time()
-        dec.load(s)
-        torch.cuda.synchronize()
-        load_ms = (time.time() - t1) * 1e3
-        del s
-        if not args.no_e2e:
-            e2e_img = img
-        del img
-    else:
-        port = os.environ.get("MASTER_PORT", "0")
-        # the stream file: about the input size (r >= 0 codes average <= 8.1 bits a byte)
-        share_dir = gh_dist.pick_share_dir(dist, rank, int(total * 1.05) + (1 << 20), args.shm, dev)
-        path = os.path.join(share_dir, f"gh_bench_{port}_{args.workload}_{per_gpu}_{world}.huff")
-        if rank == 0 and share_dir != args.shm:
-            log(f"[rank 0] {args.shm} lacks room for the stream: using {share_dir}")
-
-        def make_image():
-            d = gh.generate(args.seed, r, total, threads=threads)
-            return gh.encode(d, threads=threads)
-
-        try:
-            hdr = gh_dist.share_stream(dist, rank, path, make_image, dev)
-            b, e = gh_dist.shard_range(hdr["g"], world, rank)
-            t1 = time.time()
-            dec.load_file(path, b, e)
-            torch.cuda.synchronize()
-            load_ms = (time.time() - t1) * 1e3
-            dist.barrier()
-        finally:  # never leave the stream in RAM-backed tmpfs, whatever failed
-            if rank == 0:
-                for f in (path, path + ".part"):
-                    try:
-                        os.unlink(f)
-                    except OSError:
-                        pass
-    log(f"[rank {rank}] N={hdr['n']} W={hdr['w']} G={hdr['g']} v{hdr['version']} shard=[{b},{e}) "
-        f"setup {t1 - t0:.1f}s load {load_ms:.1f} ms")
+    res = run_workload(args, args.workload, per_gpu, r, ctx, keep_image=not use_dist and not args.no_e2e)
+    e2e_img = res.pop("image")
+    rep, alg, kern_ms = res["rep"], res["alg"], res["kern_ms"]
+    hdr, shard_bytes = res["hdr"], int(res["rep"].out_bytes)
+    ok = res["ok"]
 
     stream = torch.cuda.current_stream().cuda_stream
-    for _ in range(args.warmup):
-        dec.decode(stream, timed=False)
-    rep0 = dec.report(stream)  # synchronises, checks status of the warmup launches
-    dec.reset_timing()
-
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
-    barrier()
-    torch.cuda.synchronize()
-    ts = time.perf_counter()
-    for _ in range(args.steps):
-        dec.decode(stream, timed=True)
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - ts
-    barrier()
-    rep = dec.report(stream)
-    shard_bytes = int(rep.out_bytes)
-
-    alg = gh_dist.shard_alg_bytes(hdr["w"], b, e, shard_bytes)
-    kern_ms = float(rep.kernel_ms)
-    mx, sm = gh_dist.reduce_max_sum(dist, [elapsed, kern_ms, float(shard_bytes)], dev)
-    max_elapsed, max_kern, sum_bytes = mx[0], mx[1], sm[2]
-
-    # ---- correctness: each shard vs the generator's slice at its output offset
-    off, sizes = gh_dist.exclusive_offsets(dist, shard_bytes, dev)
-    out = torch.empty(max(1, shard_bytes), dtype=torch.uint8, device=dev)
-    dec.copy_output(out.data_ptr(), shard_bytes, 0, stream)
-    torch.cuda.synchronize()
-    ok = (sum(sizes) == hdr["n"]) and gh_dist.verify_slice(out[:shard_bytes].cpu().numpy(), args.seed, r, off,
-                                                           threads=threads)
-    status_ok = rep.status == 0 and rep0.status == 0
-    gather_ms = None
-    gather_ok = None
-    if dist is not None and not args.no_gather:
-        full, gather_ms = gh_dist.gather_to_root(dist, out, shard_bytes, dev)
-        if rank == 0:
-            gather_ok = full is not None and full.numel() == hdr["n"]
-            for k in range(world):  # gathered shard k == generator slice, compared on the GPU
-                if not gather_ok:
-                    break
-                lo = sum(sizes[:k])
-                want = torch.from_numpy(gh.generate(args.seed, r, sizes[k], offset=lo, threads=threads)).to(dev)
-                gather_ok = bool(torch.equal(full[lo:lo + sizes[k]], want))
-                del want
-            del full
-        ok = ok and (gather_ok is not False)
-    ok = gh_dist.all_true(dist, bool(ok and status_ok), dev)
-
     copy_gbps = None
     if rank == 0 and not args.no_copy:
-        del out
-        torch.cuda.empty_cache()
         try:
             copy_gbps = copy_yardstick(alg, stream, dev)
         except Exception as ex:  # the yardstick must not hide the decode number
@@ -392,18 +439,35 @@ def main() -> int:
             e2e = {"error": str(ex)[:300]}
         del e2e_img
 
+    # the second workload (default configs[4]'s r=0.5 stream: 1 GB per GPU, RCCL gather)
+    sub = None
+    if args.sub != "none" and args.sub != args.workload:
+        s_per_gpu, s_r, s_desc = WORKLOADS[args.sub]
+        if args.size:
+            s_per_gpu = args.size
+        try:
+            sres = run_workload(args, args.sub, s_per_gpu, s_r, ctx, keep_image=False)
+            if rank == 0:
+                sub = sub_record(args, args.sub, sres, s_r, s_desc, s_per_gpu)
+            ok = ok and sres["ok"]
+        except Exception as ex:  # reported; a failed sub-record fails the run
+            log(f"[rank {rank}] sub-workload {args.sub} failed: {ex}")
+            sub = {"workload": args.sub, "error": str(ex)[:300], "bitexact": False}
+            ok = False
+        ok = gh_dist.all_true(dist, bool(ok), dev)
+
     if rank == 0:
         achieved = alg / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
         read_bytes = alg - shard_bytes
         traffic, tsrc = load_traffic(args.workload, per_gpu, world)
         line = {
             "metric": "decoded GB/s",
-            "value": round(sum_bytes * args.steps / max_elapsed / 1e9, 3),
+            "value": round(res["sum_bytes"] * args.steps / res["max_elapsed"] / 1e9, 3),
             "unit": "GB/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(max_elapsed / args.steps * 1e3, 4),
+            "ms_per_step": round(res["max_elapsed"] / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -411,7 +475,7 @@ def main() -> int:
             "data": f"synthetic: seeded generate.cpp distribution (redundancy {r}), encoded by the "
                     f"in-repo gap-array encoder (reference boundary_PM code lengths)",
             "config": {"workload": args.workload, "description": desc, "bytes_per_gpu": per_gpu,
-                       "global_bytes": total, "redundancy": r, "compressed_bytes": hdr["file_bytes"],
+                       "global_bytes": res["total"], "redundancy": r, "compressed_bytes": hdr["file_bytes"],
                        "format_version": hdr["version"], "segments": hdr["g"],
                        "parallelism": f"gap-segment shards x{world}",
                        "lut_bits": int(rep.lut_bits), "grid": int(rep.grid)},
@@ -426,18 +490,19 @@ def main() -> int:
                                                     KERNEL_NAMES.get((int(rep.mode), -1))),
                          "mode": gh.MODE_NAMES.get(int(rep.mode)),
                          "path": gh.PATH_NAMES.get(int(rep.path)),
-                         "kernel_ms": round(kern_ms, 4), "max_kernel_ms_over_ranks": round(max_kern, 4),
+                         "kernel_ms": round(kern_ms, 4), "max_kernel_ms_over_ranks": round(res["max_kern"], 4),
                          "alg_bytes_per_launch": alg,
                          "traffic_source": tsrc},
-            "bitexact": bool(ok),
-            "gather_ms": None if gather_ms is None else round(gather_ms, 3),
-            "gather_bitexact": gather_ok,
-            "load_ms": round(load_ms, 2),
+            "bitexact": bool(res["ok"]),
+            "gather_ms": None if res["gather_ms"] is None else round(res["gather_ms"], 3),
+            "gather_bitexact": res["gather_ok"],
+            "load_ms": round(res["load_ms"], 2),
             "load_kind": "host memory -> HBM (pageable)" if not use_dist else
-                         f"gh_ctx_load_file: {share_dir} file -> pinned -> HBM, shard words only",
+                         f"gh_ctx_load_file: {res['share_dir']} file -> pinned -> HBM, shard words only",
             "dist": {"backend": "nccl (RCCL)", "world": world, "forced": bool(args.force_dist and world == 1),
-                     "share_dir": share_dir} if use_dist else None,
+                     "share_dir": res["share_dir"]} if use_dist else None,
             "e2e": e2e,
+            "sub": sub,
         }
         if world == 1 and not use_dist and args.cpu_sample > 0:
             try:
@@ -449,7 +514,6 @@ def main() -> int:
         if args.out_json:
             with open(args.out_json, "w") as f:
                 f.write(json.dumps(line) + "\n")
-    dec.close()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

@@ -25,6 +25,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "gh_device.hpp"
@@ -476,9 +477,13 @@ extern "C" int gh_ctx_load(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e
   const uint64_t alloc_words = 4 * c->nseg + 16;
   GH_HIP(hipMalloc(&c->d_payload, 4 * alloc_words));
   GH_HIP(hipMemset(c->d_payload, 0, 4 * alloc_words));
-  if (have)
-    GH_HIP(hipMemcpy(c->d_payload, (const uint8_t*)s->payload + 4 * w0, 4 * have,
-                     hipMemcpyHostToDevice));
+  if (have) {
+    if (use_staged(4 * have)) {  // pinned double-buffered (concurrent across shards' threads)
+      if (int rc2 = h2d_staged(c->device, (const uint8_t*)s->payload + 4 * w0, 4 * have, c->d_payload)) return rc2;
+    } else {
+      GH_HIP(hipMemcpy(c->d_payload, (const uint8_t*)s->payload + 4 * w0, 4 * have, hipMemcpyHostToDevice));
+    }
+  }
   // gap nibbles: starts of local segments 1..nseg-1 and ends of all: global [b-1, e)
   const uint64_t gw0 = b >> 3;
   const uint64_t gw1 = (e >= 1) ? ((e - 1) >> 3) + 1 : gw0 + 1;
@@ -748,6 +753,7 @@ extern "C" int gh_ctx_download(gh_ctx* c, uint64_t off, uint8_t* dst, uint64_t n
   if (!nbytes) return GH_OK;
   GH_HIP(hipSetDevice(c->device));
   if (int rc = wait_decode(c)) return rc;
+  if (use_staged(nbytes)) return d2h_staged(c->device, c->d_out + off, nbytes, dst);
   GH_HIP(hipMemcpy(dst, c->d_out + off, nbytes, hipMemcpyDeviceToHost));
   return GH_OK;
 }
@@ -771,6 +777,38 @@ extern "C" int gh_ctx_copy_output(gh_ctx* c, uint64_t off, void* dst, uint64_t n
   return GH_OK;
 }
 
+// Decode time of a set of shards: decodes on one device run in turn (DevChain), so a
+// device's time is the sum of its shards' kernel times; devices run side by side.
+static float shards_kernel_ms(const std::vector<gh_ctx*>& ctx, const std::vector<gh_report>& reps) {
+  std::map<int, float> per_dev;
+  for (size_t k = 0; k < ctx.size(); ++k) per_dev[ctx[k]->device] += reps[k].kernel_ms;
+  float worst = 0;
+  for (auto& d : per_dev) worst = std::max(worst, d.second);
+  return worst;
+}
+
+// Runs f(k) for every shard k in its own host thread (one shard alone: inline);
+// returns the first failure's code with its message moved to the calling thread.
+template <class F>
+static int for_each_shard(int n, F f) {
+  if (n == 1) return f(0);
+  std::vector<int> rc(n, GH_OK);
+  std::vector<std::string> msg(n);
+  std::vector<std::thread> th;
+  for (int k = 0; k < n; ++k)
+    th.emplace_back([&, k] {
+      rc[k] = f(k);
+      if (rc[k]) msg[k] = gh_last_error();
+    });
+  for (auto& t : th) t.join();
+  for (int k = 0; k < n; ++k)
+    if (rc[k]) {
+      set_error(msg[k]);
+      return rc[k];
+    }
+  return GH_OK;
+}
+
 extern "C" int gh_decode(const gh_stream* s, uint8_t* out, uint64_t out_len, const gh_opts* o,
                          gh_report* rep) {
   if (!s || (s->n && !out)) return fail(GH_E_ARG, "null argument");
@@ -785,50 +823,47 @@ extern "C" int gh_decode(const gh_stream* s, uint8_t* out, uint64_t out_len, con
   auto cleanup = [&]() {
     for (auto* c : ctx) gh_ctx_destroy(c);
   };
-  for (int k = 0; k < ng; ++k) {
-    const int dev = (o && o->devices) ? o->devices[k] : (ng > 1 ? k : 0);
-    rc = gh_ctx_create(dev, &ctx[k]);
-    if (!rc) rc = gh_ctx_load(ctx[k], s, bounds[k], bounds[k + 1], ng > 1 ? 0 : s->n);
-    if (rc) {
-      cleanup();
-      return rc;
-    }
-  }
-  for (int r = 0; r < reps; ++r)
-    for (int k = 0; k < ng; ++k)
-      if ((rc = gh_ctx_decode(ctx[k], nullptr, 1))) {
-        cleanup();
-        return rc;
-      }
+  // Phase 1, one host thread per shard: context, H2D of the shard's words (pinned,
+  // double-buffered: the shards' PCIe transfers overlap across devices), the decodes
+  // (chained per device), the report.  The reference loads, decodes and downloads one
+  // device at a time (decoder.cu:759-801).
   std::vector<gh_report> reps_k(ng);
-  uint64_t offset = 0;
+  rc = for_each_shard(ng, [&](int k) {
+    const int dev = (o && o->devices) ? o->devices[k] : (ng > 1 ? k : 0);
+    int r = gh_ctx_create(dev, &ctx[k]);
+    if (!r) r = gh_ctx_load(ctx[k], s, bounds[k], bounds[k + 1], ng > 1 ? 0 : s->n);
+    for (int i = 0; i < reps && !r; ++i) r = gh_ctx_decode(ctx[k], nullptr, 1);
+    if (!r) r = gh_ctx_report(ctx[k], nullptr, &reps_k[k]);
+    return r;
+  });
+  if (rc) {
+    cleanup();
+    return rc;
+  }
+  // output offsets: exclusive scan of the shards' symbol counts
+  std::vector<uint64_t> offs(ng + 1, 0), want(ng, 0);
   uint32_t status = 0;
-  float worst_ms = 0;
   for (int k = 0; k < ng; ++k) {
-    if ((rc = gh_ctx_report(ctx[k], nullptr, &reps_k[k]))) {
-      cleanup();
-      return rc;
-    }
     status |= reps_k[k].status;
-    worst_ms = std::max(worst_ms, reps_k[k].kernel_ms);
-    const uint64_t want = (offset < s->n) ? std::min<uint64_t>(reps_k[k].symbols, s->n - offset) : 0;
     if (k + 1 < ng && reps_k[k].symbols > reps_k[k].out_bytes) {
       cleanup();
       return fail(GH_E_CORRUPT, "shard produced more symbols than its output capacity");
     }
-    if (want && (rc = gh_ctx_download(ctx[k], 0, out + offset, want))) {
-      cleanup();
-      return rc;
-    }
-    offset += reps_k[k].symbols;
+    want[k] = (offs[k] < s->n) ? std::min<uint64_t>(reps_k[k].symbols, s->n - offs[k]) : 0;
+    offs[k + 1] = offs[k] + reps_k[k].symbols;
   }
+  const uint64_t offset = offs[ng];
+  // Phase 2, one host thread per shard: D2H into the caller's buffer at its offset.
+  rc = for_each_shard(ng, [&](int k) { return want[k] ? gh_ctx_download(ctx[k], 0, out + offs[k], want[k]) : GH_OK; });
+  const float dec_ms = shards_kernel_ms(ctx, reps_k);
   cleanup();
+  if (rc) return rc;
   if (rep) {
     *rep = reps_k[0];
     rep->symbols = offset;
     rep->out_bytes = std::min<uint64_t>(offset, s->n);
     rep->status = status;
-    rep->kernel_ms = worst_ms;
+    rep->kernel_ms = dec_ms;
   }
   if (status & GH_ST_TIMEOUT) return fail(GH_E_HIP, "look-back timed out");
   if (offset < s->n) return fail(GH_E_CORRUPT, "stream decoded to fewer than N symbols");

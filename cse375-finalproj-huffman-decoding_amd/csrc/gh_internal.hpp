@@ -54,4 +54,13 @@ int plan_from_counts(gh_encode_plan* plan, int force_version);
 // Writes the image header; returns its size.  out must hold file_bytes - payload.
 size_t encode_header(const gh_encode_plan* plan, uint8_t* out);
 
+// Host memory <-> device memory through the device's pinned staging buffers
+// (gh_io.cpp): each 32 MiB chunk is copied to / from a pinned buffer by a few host
+// threads while the DMA of the previous chunk runs (hipMemcpyAsync), so shards on
+// different devices, loaded from different host threads, move concurrently.
+int h2d_staged(int device, const void* src, uint64_t n, void* dst);
+int d2h_staged(int device, const void* src, uint64_t n, void* dst);
+// Large copies go through the staging unless GH_H2D=pageable (measurements).
+bool use_staged(uint64_t n);
+
 }  // namespace gh

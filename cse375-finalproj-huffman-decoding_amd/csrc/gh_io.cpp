@@ -88,9 +88,11 @@ struct Staging {
 };
 
 std::mutex g_pool_mu;
-std::map<int, Staging*> g_pool;  // device -> idle staging set (never freed)
+std::map<int, std::vector<Staging*>> g_pool;  // device -> idle staging sets (never freed)
+constexpr size_t POOL_KEEP = 8;  // idle sets kept per device (concurrent shards on one device)
 
-// Takes the device's staging set (or makes one) for the duration of a call.
+// Takes an idle staging set of the device (or makes one) for the duration of a call;
+// concurrent calls on one device (shards in host threads) each get their own.
 struct StagingLease {
   int dev;
   Staging* s = nullptr;
@@ -98,10 +100,10 @@ struct StagingLease {
   int acquire() {
     {
       std::lock_guard<std::mutex> g(g_pool_mu);
-      auto it = g_pool.find(dev);
-      if (it != g_pool.end() && it->second) {
-        s = it->second;
-        it->second = nullptr;
+      auto& v = g_pool[dev];
+      if (!v.empty()) {
+        s = v.back();
+        v.pop_back();
       }
     }
     if (!s) s = new Staging();
@@ -110,9 +112,9 @@ struct StagingLease {
   ~StagingLease() {
     if (!s) return;
     std::lock_guard<std::mutex> g(g_pool_mu);
-    Staging*& slot = g_pool[dev];
-    if (!slot && s->ready()) {
-      slot = s;  // keep one complete set per device
+    auto& v = g_pool[dev];
+    if (v.size() < POOL_KEEP && s->ready()) {
+      v.push_back(s);
     } else {
       s->release();
       delete s;
@@ -185,6 +187,69 @@ struct DevMem {
 };
 
 }  // namespace
+
+bool use_staged(uint64_t n) {
+  static const bool pageable = [] {
+    const char* e = getenv("GH_H2D");
+    return e && !strcmp(e, "pageable");
+  }();
+  return !pageable && n >= (8u << 20);
+}
+
+// Host bytes -> device, double-buffered: the host copy of chunk c+1 (split over
+// IO_THREADS threads) overlaps the DMA of chunk c.
+int h2d_staged(int device, const void* src, uint64_t n, void* dst) {
+  GH_HIPI(hipSetDevice(device));
+  StagingLease lease(device);
+  int rc = lease.acquire();
+  if (rc) return rc;
+  Staging& s = *lease.s;
+  int b = 0;
+  for (uint64_t done = 0; done < n; b ^= 1) {
+    const size_t c = (size_t)std::min<uint64_t>(IO_CHUNK, n - done);
+    GH_HIPI(hipEventSynchronize(s.ev[b]));  // the DMA that last used this buffer
+    uint8_t* hb = (uint8_t*)s.buf[b];
+    const uint8_t* sp = (const uint8_t*)src + done;
+    par_io(c, [&](size_t a, size_t m) { std::memcpy(hb + a, sp + a, m); return true; });
+    GH_HIPI(hipMemcpyAsync((uint8_t*)dst + done, hb, c, hipMemcpyHostToDevice, s.st));
+    GH_HIPI(hipEventRecord(s.ev[b], s.st));
+    done += c;
+  }
+  GH_HIPI(hipStreamSynchronize(s.st));
+  return GH_OK;
+}
+
+// Device bytes -> host: the DMA of chunk c+1 overlaps the host copy of chunk c.
+int d2h_staged(int device, const void* src, uint64_t n, void* dst) {
+  GH_HIPI(hipSetDevice(device));
+  StagingLease lease(device);
+  int rc = lease.acquire();
+  if (rc) return rc;
+  Staging& s = *lease.s;
+  uint64_t pend_off = 0;
+  size_t pend_n = 0;
+  int pend_b = -1, b = 0;
+  for (uint64_t done = 0;; b ^= 1) {
+    const size_t c = (size_t)std::min<uint64_t>(IO_CHUNK, n - done);
+    if (c) {
+      GH_HIPI(hipMemcpyAsync(s.buf[b], (const uint8_t*)src + done, c, hipMemcpyDeviceToHost, s.st));
+      GH_HIPI(hipEventRecord(s.ev[b], s.st));
+    }
+    if (pend_b >= 0) {
+      GH_HIPI(hipEventSynchronize(s.ev[pend_b]));
+      const uint8_t* hb = (const uint8_t*)s.buf[pend_b];
+      uint8_t* dp = (uint8_t*)dst + pend_off;
+      par_io(pend_n, [&](size_t a, size_t m) { std::memcpy(dp + a, hb + a, m); return true; });
+    }
+    if (!c) break;
+    pend_b = b;
+    pend_off = done;
+    pend_n = c;
+    done += c;
+  }
+  return GH_OK;
+}
+
 }  // namespace gh
 
 using namespace gh;

@@ -227,7 +227,7 @@ __device__ __forceinline__ uint32_t stage_aligned_p1(const uint32_t (&ow)[OW], u
     const uint32_t r = __builtin_amdgcn_alignbyte(hi, ow[m - 1], s);
     if ((uint32_t)m <= last) lds_st32(base + 4u * m, r);
   }
-  return 4u - ap;
+  return min(4u - ap, n);  // (n >= 4 - ap for every grouped code; never write past n)
 }
 // Phase 2: the nb (1..3) head bytes h at o (o + (nb & 1) is even).
 __device__ __forceinline__ void stage_head(uint32_t o, uint32_t h, uint32_t nb) {
@@ -491,19 +491,21 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE,
     // ---- copy tile k-2 out (its prefix was published about an iteration ago) ----------
     if (have2) {
       unsigned long long goff = 0;
-      bool polled = false;
+      bool polled = false, got = true;
       if (lane == 0) {
         polled = !granule_ok(p, gp, 2);
         if (polled) {
           if (wid == 0) atomicAdd(p.stats, 1ull);
           gp = poll_granule(p, &p.prefix[t2], 2);
+          got = granule_ok(p, gp, 2);  // false only after a timeout (then nothing is written)
         }
         goff = gp & GRAN_VMASK;
-        if (wid == 0 && t2 == p.ntiles - 1) *p.total = goff + tot2;
+        if (wid == 0 && t2 == p.ntiles - 1 && got) *p.total = goff + tot2;
       }
       goff = rfl_u64(goff);
       ahead = __builtin_amdgcn_readfirstlane(polled ? 1 : 0) != 0;
-      const uint32_t n2 = goff >= p.out_cap ? 0u : (uint32_t)min<unsigned long long>(tot2, p.out_cap - goff);
+      got = __builtin_amdgcn_readfirstlane(got ? 1 : 0) != 0;
+      const uint32_t n2 = (!got || goff >= p.out_cap) ? 0u : (uint32_t)min<unsigned long long>(tot2, p.out_cap - goff);
       load(nxt);  // the next tile's words, issued before this copy-out's stores
       copy_out_tile<TB, TILE_NS>(p.out, p.lut_bytes + buf * p.stage_bytes, goff, n2, tid,
                                  p.junk + (unsigned long long)blockIdx.x * TB + tid);
@@ -527,15 +529,19 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE,
     const bool staged = have_cur && tile_total + (uint32_t)(STAGE_PAD + 48) <= p.stage_bytes;
     if (have_cur && !staged) {
       unsigned long long goff = 0;
+      bool got = true;
       if (lane == 0) {
         unsigned long long g = __hip_atomic_load(&p.prefix[cur], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (!granule_ok(p, g, 2)) g = poll_granule(p, &p.prefix[cur], 2);
+        got = granule_ok(p, g, 2);  // false only after a timeout (then nothing is written)
         goff = g & GRAN_VMASK;
-        if (wid == 0 && cur == p.ntiles - 1) *p.total = goff + tile_total;
+        if (wid == 0 && cur == p.ntiles - 1 && got) *p.total = goff + tile_total;
       }
       goff = rfl_u64(goff);
+      if (__builtin_amdgcn_readfirstlane(got ? 1 : 0)) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) store_direct(p.out, p.out_cap, goff + bpos[u], ow[u], cnt[u]);
+        for (int u = 0; u < U; ++u) store_direct(p.out, p.out_cap, goff + bpos[u], ow[u], cnt[u]);
+      }
     } else if (have_cur) {
       // stage this tile into buffer k & 1 (copied out two iterations later) at its
       // absolute LDS address (the kernel's LDS starts at 0)

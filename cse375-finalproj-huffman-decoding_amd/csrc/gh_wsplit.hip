@@ -238,7 +238,11 @@ __global__ __launch_bounds__(TBK) void gh_ws_count_kernel(const WsParams p) {
           for (int u = 0; u < U; ++u) {
             if constexpr (FB) {
               if ((e[u] & 0xFFFFu) == 0u) {
-                const uint32_t l = ws_canon(s_fb, xs[u] >> 16, p.fb_lo, p.fb_hi, bad) & 31u;
+                // only a lookup that starts before the segment end may flag the stream
+                // (lanes past the shard end and finished segments decode stray bits)
+                uint32_t b1 = 0;
+                const uint32_t l = ws_canon(s_fb, xs[u] >> 16, p.fb_lo, p.fb_hi, b1) & 31u;
+                bad |= ((int)(0u - q[u]) < R[u]) ? b1 : 0u;
                 e[u] = l | ((1u << (l - 1u)) << 16);
               }
             }
@@ -454,7 +458,9 @@ __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
             for (int u = 0; u < U; ++u) {
               if constexpr (FB) {
                 if ((e[u].y & 0x700u) == 0u) {  // n = 0
-                  const uint32_t r = ws_canon(s_fb, xs[u] >> 16, p.fb_lo, p.fb_hi, bad);
+                  uint32_t b1 = 0;  // flags only a lookup whose symbol is written
+                  const uint32_t r = ws_canon(s_fb, xs[u] >> 16, p.fb_lo, p.fb_hi, b1);
+                  bad |= ptr[u] < end[u] ? b1 : 0u;
                   e[u] = make_uint2(r >> 8, (r & 31u) | (1u << 8));
                 }
               }

@@ -17,7 +17,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "gaphuff.h"
@@ -25,6 +27,28 @@
 static double now_ms() {
   using namespace std::chrono;
   return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
+}
+
+// Runs f(k) for every shard in its own host thread; the first failure's code, with its
+// message re-raised on the calling thread (gh_last_error is per thread).
+template <class F>
+static int for_each_shard(int n, F f) {
+  if (n == 1) return f(0);
+  std::vector<int> rc(n, GH_OK);
+  std::vector<std::string> msg(n);
+  std::vector<std::thread> th;
+  for (int k = 0; k < n; ++k)
+    th.emplace_back([&, k] {
+      rc[k] = f(k);
+      if (rc[k]) msg[k] = gh_last_error();
+    });
+  for (auto& t : th) t.join();
+  for (int k = 0; k < n; ++k)
+    if (rc[k]) {
+      std::fprintf(stderr, "decoder: shard %d: %s\n", k, msg[k].c_str());
+      return rc[k];
+    }
+  return GH_OK;
 }
 
 static int die(const char* what, int rc) {
@@ -117,12 +141,14 @@ int main(int argc, char** argv) {
       return die("bad compressed stream / upload", rc);
     }
     gh_plan_shards(info.g, (uint32_t)nshards, bounds.data());
-    for (int k = 0; k < nshards; ++k) {
-      if (k && (rc = gh_ctx_create(k % ngpus, &ctx[k]))) { cleanup(); return die("device init", rc); }
-      if ((rc = gh_ctx_load_file(ctx[k], argv[1], bounds[k], bounds[k + 1], 0, nullptr))) {
-        cleanup();
-        return die("upload", rc);
-      }
+    // one host thread per shard: each streams its own payload range through its own
+    // pinned buffers, so the shards' file reads and H2D transfers overlap
+    if ((rc = for_each_shard(nshards, [&](int k) {
+           int r = k ? gh_ctx_create(k % ngpus, &ctx[k]) : GH_OK;
+           return r ? r : gh_ctx_load_file(ctx[k], argv[1], bounds[k], bounds[k + 1], 0, nullptr);
+         }))) {
+      cleanup();
+      return die("upload", rc);
     }
   }
   s.n = info.n;
@@ -136,15 +162,19 @@ int main(int argc, char** argv) {
     for (int k = 0; k < nshards; ++k)
       if ((rc = gh_ctx_decode(ctx[k], nullptr, 1))) { cleanup(); return die("decode", rc); }
   std::vector<gh_report> rep(nshards);
-  float dec_ms = 0;
   uint32_t status = 0;
   uint64_t total = 0;
+  std::map<int, float> dev_ms;  // decodes on one device run in turn: their times add up
   for (int k = 0; k < nshards; ++k) {
     if ((rc = gh_ctx_report(ctx[k], nullptr, &rep[k]))) { cleanup(); return die("decode", rc); }
-    dec_ms = std::max(dec_ms, rep[k].kernel_ms);
+    int dev = 0;
+    gh_ctx_device(ctx[k], &dev);
+    dev_ms[dev] += rep[k].kernel_ms;
     status |= rep[k].status;
     total += rep[k].symbols;
   }
+  float dec_ms = 0;  // devices run side by side
+  for (auto& d : dev_ms) dec_ms = std::max(dec_ms, d.second);
   if (status) {
     cleanup();
     std::fprintf(stderr, "decoder: device reported status 0x%x (corrupted stream?)\n", status);
@@ -158,19 +188,30 @@ int main(int argc, char** argv) {
   // each shard writes its bytes at its offset of argv[2] (pinned double-buffered
   // D2H -> pwrite); the reference always wrote "decodedfile" (huff.cpp:32)
   const double t2 = now_ms();
-  uint64_t off = 0;
+  std::vector<uint64_t> off(nshards + 1, 0), want(nshards, 0);
   for (int k = 0; k < nshards; ++k) {
     if (k + 1 < nshards && rep[k].symbols > rep[k].out_bytes) {
       cleanup();
       std::fprintf(stderr, "decoder: shard %d overflowed its output (corrupted stream?)\n", k);
       return 1;
     }
-    const uint64_t want = off < s.n ? std::min<uint64_t>(rep[k].symbols, s.n - off) : 0;
-    if ((rc = gh_ctx_save_file(ctx[k], argv[2], off, 0, want, k == 0, nullptr))) {
+    want[k] = off[k] < s.n ? std::min<uint64_t>(rep[k].symbols, s.n - off[k]) : 0;
+    off[k + 1] = off[k] + rep[k].symbols;
+  }
+  {  // create / truncate the output once, then every shard writes its range concurrently
+    FILE* f = std::fopen(argv[2], "wb");
+    if (!f) {
       cleanup();
-      return die("write output", rc);
+      std::fprintf(stderr, "decoder: cannot create %s\n", argv[2]);
+      return 1;
     }
-    off += rep[k].symbols;
+    std::fclose(f);
+  }
+  if ((rc = for_each_shard(nshards, [&](int k) {
+         return gh_ctx_save_file(ctx[k], argv[2], off[k], 0, want[k], 0, nullptr);
+       }))) {
+    cleanup();
+    return die("write output", rc);
   }
   const double t3 = now_ms();
   cleanup();

@@ -264,8 +264,13 @@ int gh_ctx_load_raw(gh_ctx* ctx, const gh_sym* syms, uint32_t nsyms, uint64_t n,
 /* One-shot decode of a whole stream into host memory `out` (out_len >= N):
  * mirrors decoder_l1_l2 (decoder.cu:732-815) without its 200-iteration loop.
  * ngpus <= 0 or 1: device `devices ? devices[0] : 0`; ngpus > 1 shards the
- * segments evenly over `devices` (or 0..ngpus-1), decodes each shard on its own
- * device, and places shard outputs at the scanned offsets. */
+ * segments evenly over `devices` (or 0..ngpus-1; a device may repeat), decodes each
+ * shard on its own device, and places shard outputs at the scanned offsets.  Each
+ * shard is loaded, decoded and downloaded from its own host thread through pinned
+ * double-buffered copies, so the shards' PCIe transfers overlap across devices (the
+ * reference's launcher runs one device after another, decoder.cu:759-801).
+ * rep->kernel_ms: per device the SUM of its shards' average decode times (decodes on
+ * one device run in turn), the maximum over devices. */
 typedef struct gh_opts {
   int ngpus;
   const int* devices;

@@ -208,6 +208,9 @@ def test_bench_contract_small(gpu):
         assert k in j
     assert j["bitexact"] is True and j["value"] > 0
     assert 0 < j["roofline"]["frac"] < 1
+    sub = j["sub"]  # configs[4]'s r=0.5 stream, timed in the same run
+    assert sub["workload"] == "cfg5" and sub["redundancy"] == 0.5 and sub["bitexact"] is True
+    assert sub["value"] > 0 and 0 < sub["roofline_frac"] < 1
 
 
 @pytest.mark.gpu

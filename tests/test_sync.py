@@ -265,6 +265,21 @@ def test_gpu_sync_random_codes(gpu, orc, seed):
     assert np.array_equal(gpu.decode_raw(units, syms, n), d)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [100_003, 8_191, 1_000_001])
+def test_gpu_incomplete_code_large_unused_region(gpu, orc, n):
+    """A code with a quarter of its code space unused ('11' of three 2-bit codewords):
+    lanes past the shard end and segments past their end decode stray bits that hit
+    the unused pattern; only lookups of kept codewords may flag the stream as corrupt
+    (the wave split's canonical fallback).  nseg is not a multiple of a block."""
+    syms = [(65, 2), (66, 2), (67, 2)]
+    rng = np.random.default_rng(n)
+    d = np.array([65, 66, 67], dtype=np.uint8)[rng.integers(0, 3, n)]
+    units = orc.raw_encode(d, syms)
+    assert (2 * n + 127) // 128 % 256 != 0
+    assert np.array_equal(gpu.decode_raw(units, syms, n), d)
+
+
 BIN = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bin")
 
 
