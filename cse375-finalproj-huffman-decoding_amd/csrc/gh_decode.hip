@@ -50,10 +50,20 @@ using namespace gh;
       return fail(GH_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));   \
   } while (0)
 
-static const void* tile_kernel_for(uint32_t g) {
-  return g >= 4 ? (const void*)gh_tile_kernel<TILE_TB, TILE_U, 4>
-       : g == 3 ? (const void*)gh_tile_kernel<TILE_TB, TILE_U, 3>
-                : (const void*)gh_tile_kernel<TILE_TB, TILE_U, 2>;
+// Tile kernel shapes: codes of >= 4-bit codewords (at most 32 per segment) run three
+// segments per lane with 8 output words each; codes with 3-bit codewords (at most 43
+// per segment, e.g. BASELINE's r = 0.5 codes) two segments per lane with 11 words (the
+// registers and the staging of a third segment would halve the workgroups per CU).
+constexpr uint32_t TILE_U3 = 2;  // segments per lane, minlen-3 codes
+static uint32_t tile_u_for(uint32_t minlen) { return minlen >= 4 ? (uint32_t)TILE_U : TILE_U3; }
+static const void* tile_kernel_for(uint32_t minlen, uint32_t g) {
+  if (minlen >= 4)
+    return g >= 4 ? (const void*)gh_tile_kernel<TILE_TB, TILE_U, 4, 8, 4>
+         : g == 3 ? (const void*)gh_tile_kernel<TILE_TB, TILE_U, 3, 8, 4>
+                  : (const void*)gh_tile_kernel<TILE_TB, TILE_U, 2, 8, 4>;
+  return g >= 4 ? (const void*)gh_tile_kernel<TILE_TB, TILE_U3, 4, 11, 3>
+       : g == 3 ? (const void*)gh_tile_kernel<TILE_TB, TILE_U3, 3, 11, 3>
+                : (const void*)gh_tile_kernel<TILE_TB, TILE_U3, 2, 11, 3>;
 }
 
 struct WsKernels {
@@ -105,6 +115,7 @@ struct gh_ctx {
   // tile kernel (grouped codes)
   bool tile = false;
   uint32_t tile_k = 0, tile_g = 0, lgr = 0;  // LUT width, codewords per window shift, log2 LUT copies
+  uint32_t tile_minl = 4, tile_u = TILE_U;     // kernel shape (tile_kernel_for), segments per lane
   uint32_t* d_lut_t = nullptr;
   uint4* d_tile_junk = nullptr;    // one 16-byte slot per thread of the grid
   unsigned long long* d_gran = nullptr;  // granules, within-round prefixes, round starts
@@ -159,21 +170,26 @@ static void free_shard(gh_ctx* c) {
 // LUT width K (>= maxlen), replicated 2^lgr times in LDS: the largest replication that
 // keeps the best occupancy.  Returns GH_OK with c->tile false when the kernel does not
 // fit a CU (the wave split then takes the code).
-static int tile_setup(gh_ctx* c, uint32_t K) {
+static int tile_setup(gh_ctx* c, uint32_t K, double avg_seg_bytes) {
   const Canon& cn = c->canon;
-  const uint32_t maxsyms = (128 + cn.minlen - 1) / cn.minlen;  // <= 32 (minlen >= 4)
+  const uint32_t maxsyms = (128 + cn.minlen - 1) / cn.minlen;  // <= 43 (minlen >= 3)
   c->tile_k = K;
   c->tile_g = std::min<uint32_t>(4, 32 / cn.maxlen);
-  c->ntiles = (uint32_t)ceil_div(c->nseg, (uint64_t)TILE_U * TILE_TB);
-  // Staging is sized for TILE_SCAP bytes per segment, not the worst case (128 / minlen):
-  // two workgroups per CU then fit three segments per lane.  A tile is the sum of 1536
-  // segments, so it stays near its mean (r = 0.1: 16.5 bytes per segment); a larger one
-  // stores straight from registers (gh_tile_kernel).  GH_TILE_SCAP overrides (tests).
-  uint64_t per_seg = std::min<uint64_t>(maxsyms, TILE_SCAP);
+  c->tile_minl = cn.minlen >= 4 ? 4 : 3;
+  c->tile_u = tile_u_for(cn.minlen);
+  c->ntiles = (uint32_t)ceil_div(c->nseg, (uint64_t)c->tile_u * TILE_TB);
+  // Staging is sized for the typical tile, not the worst case (128 / minlen bytes per
+  // segment): TILE_SCAP = 20 bytes per segment for grouped codes (r = 0.1: 16.5), the
+  // stream's mean + 12 % for minlen-3 codes (r = 0.5: 21.5 -> 25), so that two
+  // workgroups fit a CU.  A tile is the sum of 1024-1536 segments, so it stays near its
+  // mean; a larger one stores straight from registers (gh_tile_kernel).  GH_TILE_SCAP
+  // overrides (tests).
+  uint64_t per_seg = std::min<uint64_t>(
+      maxsyms, cn.minlen >= 4 ? (uint64_t)TILE_SCAP : (uint64_t)std::ceil(std::max(avg_seg_bytes, 1.0) * 1.12 + 1));
   if (const char* e = getenv("GH_TILE_SCAP")) per_seg = std::min<uint64_t>(maxsyms, (uint64_t)std::max(1, atoi(e)));
-  c->stage_bytes = (uint32_t)((STAGE_PAD + (uint64_t)TILE_U * TILE_TB * per_seg + 48 + 127) & ~127ull);
+  c->stage_bytes = (uint32_t)((STAGE_PAD + (uint64_t)c->tile_u * TILE_TB * per_seg + 48 + 127) & ~127ull);
   const std::vector<uint32_t> lt = grouped_lut(cn, K);
-  const void* kern = tile_kernel_for(c->tile_g);
+  const void* kern = tile_kernel_for(c->tile_minl, c->tile_g);
   const char* envr = getenv("GH_LGR");
   const int lg = envr ? std::clamp(atoi(envr), 0, 14 - (int)K) : std::min(5, 14 - (int)K);
   int best = 0, best_lg = 0;
@@ -374,8 +390,9 @@ extern "C" int gh_ctx_create(int device, gh_ctx** out) {
   GH_HIP(hipEventCreateWithFlags(&c->done, hipEventDisableTiming));
   GH_HIP(hipMalloc(&c->d_misc, 128));
   GH_HIP(hipMemset(c->d_misc, 0, 128));
-  for (uint32_t gv : {2u, 3u, 4u})
-    (void)hipFuncSetAttribute(tile_kernel_for(gv), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  for (uint32_t ml : {3u, 4u})
+    for (uint32_t gv : {2u, 3u, 4u})
+      (void)hipFuncSetAttribute(tile_kernel_for(ml, gv), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   (void)hipGetLastError();
   *out = c;
   return GH_OK;
@@ -439,10 +456,11 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
     if (envm && *envm && !force_tile && !force_ws) return fail(GH_E_ARG, "GH_MODE: tile or wsplit");
     const char* envk = getenv("GH_LUT_BITS");
     const uint32_t K = envk ? (uint32_t)std::clamp(atoi(envk), 1, 12) : cn.maxlen;
-    const bool grouped = grouped_code(cn) && K >= cn.maxlen;
-    if (force_tile && !grouped) return fail(GH_E_ARG, "GH_MODE=tile: the code is not grouped (complete, 4..12 bits)");
+    const bool grouped = (grouped_code(cn) || short_code(cn)) && K >= cn.maxlen;
+    if (force_tile && !grouped)
+      return fail(GH_E_ARG, "GH_MODE=tile: the code is not for the tile kernel (complete, 3..12 bits)");
     if (grouped && !force_ws) {
-      if ((rc = tile_setup(c, K))) return rc;
+      if ((rc = tile_setup(c, K, s->g ? (double)s->n / (double)s->g : 16.0))) return rc;
       if (force_tile && !c->tile) return fail(GH_E_HIP, "GH_MODE=tile: the tile kernel does not fit a CU");
     }
     if (!c->tile && (rc = ws_setup(c, s->g ? (double)s->n / (double)s->g : 16.0))) return rc;
@@ -684,7 +702,7 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     static thread_local TileParams tp;
     tp = t;
     ta[0] = &tp;
-    GH_HIP(hipLaunchKernel(tile_kernel_for(c->tile_g), dim3(c->grid), dim3(TILE_TB), ta, c->lds, st));
+    GH_HIP(hipLaunchKernel(tile_kernel_for(c->tile_minl, c->tile_g), dim3(c->grid), dim3(TILE_TB), ta, c->lds, st));
     GH_HIP(hipEventRecord(dc.last, st));
     dc.has = true;
   }

@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <map>
 #include <mutex>
 #include <thread>
@@ -88,18 +89,26 @@ struct Staging {
 };
 
 std::mutex g_pool_mu;
+std::condition_variable g_pool_cv;
 std::map<int, std::vector<Staging*>> g_pool;  // device -> idle staging sets (never freed)
-constexpr size_t POOL_KEEP = 8;  // idle sets kept per device (concurrent shards on one device)
+std::map<int, int> g_live;                    // device -> sets checked out
+// Sets per device in use at once: two double-buffered sets keep one device's PCIe link
+// busy while a third call waits; more only cost pinning (~25 ms per 64 MiB set).
+constexpr int SETS_PER_DEV = 2;
 
-// Takes an idle staging set of the device (or makes one) for the duration of a call;
-// concurrent calls on one device (shards in host threads) each get their own.
+// Takes an idle staging set of the device (or makes one, up to SETS_PER_DEV per device;
+// a further concurrent call on that device waits for one) for the duration of a call.
 struct StagingLease {
   int dev;
   Staging* s = nullptr;
+  bool counted = false;
   explicit StagingLease(int d) : dev(d) {}
   int acquire() {
     {
-      std::lock_guard<std::mutex> g(g_pool_mu);
+      std::unique_lock<std::mutex> g(g_pool_mu);
+      g_pool_cv.wait(g, [&] { return g_live[dev] < SETS_PER_DEV; });
+      ++g_live[dev];
+      counted = true;
       auto& v = g_pool[dev];
       if (!v.empty()) {
         s = v.back();
@@ -110,12 +119,19 @@ struct StagingLease {
     return s->init();
   }
   ~StagingLease() {
-    if (!s) return;
-    std::lock_guard<std::mutex> g(g_pool_mu);
-    auto& v = g_pool[dev];
-    if (v.size() < POOL_KEEP && s->ready()) {
-      v.push_back(s);
-    } else {
+    {
+      std::lock_guard<std::mutex> g(g_pool_mu);
+      if (counted) --g_live[dev];
+      if (s) {
+        auto& v = g_pool[dev];
+        if (v.size() < (size_t)SETS_PER_DEV && s->ready()) {
+          v.push_back(s);
+          s = nullptr;
+        }
+      }
+    }
+    g_pool_cv.notify_all();
+    if (s) {
       s->release();
       delete s;
     }

@@ -16,6 +16,7 @@
 #pragma once
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <vector>
 
 #include "gh_internal.hpp"
@@ -72,6 +73,18 @@ inline double multi_gain(const Canon& c, uint32_t K) {
 // average < 1.5 symbols (else the wave split's four-symbol lookups win).
 inline bool grouped_code(const Canon& c) {
   return c.nsyms > 0 && c.minlen >= 4 && c.maxlen <= 12 && kraft16(c) == 65536 && multi_gain(c, 12) < 1.5;
+}
+
+// Codes for the tile kernel's minlen-3 shape: complete, shortest codeword 3 bits (at
+// most 43 per segment), maxlen <= 12 (BASELINE's r = 0.5 codes: 3- and 8/9-bit).  One
+// codeword per lookup in one payload read beats the wave split's two passes of
+// four-symbol lookups there.  GH_TILE3=0 leaves them to the wave split.
+inline bool short_code(const Canon& c) {
+  static const bool off = [] {
+    const char* e = getenv("GH_TILE3");
+    return e && e[0] == '0';
+  }();
+  return !off && c.nsyms > 0 && c.minlen == 3 && c.maxlen <= 12 && kraft16(c) == 65536;
 }
 
 // Tile kernel LUT of width K >= maxlen: entry i = {len | sym << 8 | len << 23} of the

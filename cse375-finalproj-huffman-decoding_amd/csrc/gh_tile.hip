@@ -68,7 +68,8 @@ constexpr int TILE_SCAP = 20;        // staging bytes per segment (larger tiles 
 #endif
 constexpr int TILE_MIDG = GH_TILE_MIDG;  // decode group after which the mid-decode loads are issued
 constexpr int STAGE_PAD = 16;      // staging byte STAGE_PAD + i = tile byte i
-constexpr int OW = 8;              // output words per segment (32 codewords of >= 4 bits)
+// Output words per segment: a segment holds at most ceil(128 / minlen) codewords (8
+// words at minlen 4, 11 at minlen 3), kept in registers as OW words per chain.
 
 struct TileParams {
   const uint32_t* payload;       // local segment j owns words [4j, 4j+4); +1 look-ahead, zero padded
@@ -134,7 +135,7 @@ __device__ __forceinline__ uint32_t q_init(bool act, int start) {
 // consumed bits fit Q's low byte).  Codeword j of a segment goes to byte j of ow (v_perm,
 // static index); dead codewords go there too and are never staged.  `mid()` runs once,
 // after group MIDG (or at the end if the loop stops earlier).
-template <int G, int U, int MIDG, class Mid>
+template <int G, int U, int OW, int MINL, int MIDG, class Mid>
 __device__ __forceinline__ void decode_tile_grouped(uint32_t (&e)[U][5], const int (&start)[U],
                                                     const bool (&act)[U], uint32_t (&ow)[U][OW],
                                                     uint32_t (&cnt)[U], uint32_t amask, uint32_t laneoff,
@@ -180,12 +181,12 @@ __device__ __forceinline__ void decode_tile_grouped(uint32_t (&e)[U][5], const i
     }
     uint32_t qmin = 0xFFFFFFFFu;
     // Window word k holds e-positions [C + 32k, +32) after this shift, C = the bits
-    // consumed so far >= (gi + 1) * G * 4 (a grouped code has no codeword below 4 bits).
+    // consumed so far >= (gi + 1) * G * MINL (no codeword is shorter than MINL bits).
     // A kept codeword starts before segment bit 128, e-position 127 - start + S, and its
     // lookup reads K bits: nothing at e-position >= 157 - lgr - start is read for a kept
     // codeword, so a word lying wholly at or above 157 is no longer shifted (its stale
     // bits reach only such positions; dead codewords decode garbage, never counted).
-    const int CMIN = (gi + 1) * G * 4;  // a constant once the loop is unrolled
+    const int CMIN = (gi + 1) * G * MINL;  // a constant once the loop is unrolled
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       e[u][0] = __builtin_amdgcn_alignbit(e[u][0], e[u][1], q[u]);
@@ -216,6 +217,7 @@ __device__ __forceinline__ void lds_st32(uint32_t a, uint32_t v) {
 // skipped first dword) exactly, over the previous segment's phase-1 tail.  Every dword
 // store is aligned: unaligned ds_write_b32 measured about 3x the LDS time of aligned
 // ones with per-lane offsets like these.  Returns the number of head bytes.
+template <int OW>
 __device__ __forceinline__ uint32_t stage_aligned_p1(const uint32_t (&ow)[OW], uint32_t n, uint32_t o) {
   const uint32_t ap = ((o - 1u) & 3u) + 1u;  // 1..4: bytes from the dword base to o
   const uint32_t base = o - ap;              // dword m at base + 4m holds segment bytes [4m - ap, +4)
@@ -290,6 +292,7 @@ __device__ __forceinline__ void copy_out_tile(uint8_t* out, uint32_t stg, unsign
 
 // A segment's n bytes (ow, byte 0 first) stored to out[o, o + n), clamped at cap: the
 // path of a tile too large for staging (byte stores; rare).
+template <int OW>
 __device__ __forceinline__ void store_direct(uint8_t* out, unsigned long long cap, unsigned long long o,
                                              const uint32_t (&ow)[OW], uint32_t n) {
 #pragma unroll
@@ -381,10 +384,13 @@ __device__ __forceinline__ void tile_round_leader(const TileParams& p, uint32_t*
   }
 }
 
-// TB threads, U segments per lane, GRP codewords per window shift.  Compiled for at most
-// 4 waves per SIMD (two workgroups per CU: 128 VGPRs).
-template <int TB, int U, int GRP>
+// TB threads, U segments per lane, GRP codewords per window shift, OW output words per
+// segment, codewords of at least MINL bits.  Compiled for at most 4 waves per SIMD (two
+// workgroups per CU: 128 VGPRs).
+template <int TB, int U, int GRP, int OW, int MINL>
 __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE, GH_TILE_WPE))) void gh_tile_kernel(const TileParams p) {
+  static_assert(4 * OW >= (128 + MINL - 1) / MINL, "OW words hold every codeword a segment can start");
+  static_assert(U * (TB / 64) <= 2 * TILE_U * (TB / 64), "wave sums fit tile_lds_bytes");
   constexpr int NWAVE_T = TB / 64;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* s_stage = smem + p.lut_bytes;                        // 2 buffers
@@ -464,7 +470,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE,
         make_ewin(w[u], w4[u], start[u], S, e[u]);
       }
       if (have_cur) {
-        decode_tile_grouped<GRP, U, TILE_MIDG>(e, start, act, ow, cnt, amask, laneoff, mid);
+        decode_tile_grouped<GRP, U, OW, MINL, TILE_MIDG>(e, start, act, ow, cnt, amask, laneoff, mid);
       } else {
 #pragma unroll
         for (int u = 0; u < U; ++u) {

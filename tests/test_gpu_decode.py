@@ -114,8 +114,11 @@ def test_reference_launcher_mirror(gpu):
     assert np.array_equal(out, data)
 
 
-def test_corrupted_stream_terminates(gpu):
-    data = gpu.generate(15, 0.9, 500_000)
+@pytest.mark.parametrize("r", [0.9, 0.5, 0.1])
+def test_corrupted_stream_terminates(gpu, r):
+    """Flipped payload bytes (each structure: r = 0.9 wave split, r = 0.5 / 0.1 tile
+    kernel shapes): an error or a bounded, wrong output, never a hang or a fault."""
+    data = gpu.generate(15, r, 500_000)
     img = gpu.encode(data).copy()
     rng = np.random.default_rng(1)
     hdr = 8 + 2 * len(gpu.parse(img).symbols) + 12
@@ -333,7 +336,7 @@ def test_wave_split_count_lut_widths(gpu, orc, kc, monkeypatch):
 
 
 @pytest.mark.parametrize("mode,r,scap", [("wsplit", 0.5, None), ("wsplit", 0.9, None), ("tile", 0.1, None),
-                                         ("tile", 0.1, "4")])
+                                         ("tile", 0.1, "4"), ("tile", 0.5, None), ("tile", 0.5, "4")])
 def test_output_capacity_below_total(gpu, mode, r, scap, monkeypatch):
     """An output capacity below the stream's total (gh_ctx_load out_cap) writes exactly
     the prefix that fits: caps inside the first chunk, mid-range, at a range edge and
@@ -361,18 +364,19 @@ def test_output_capacity_below_total(gpu, mode, r, scap, monkeypatch):
                     raise AssertionError(f"{mode} grid={grid} cap={cap}: {bad.size} wrong bytes, first at {bad[0]}")
 
 
-@pytest.mark.parametrize("scap", [None, "17", "4"])
-def test_tile_staging_overflow(gpu, orc, scap, monkeypatch):
-    """The tile kernel's staging holds 20 bytes per segment (the typical tile, not the
-    worst case 128 / minlen); a tile decoding to more bytes waits for its own prefix and
-    stores straight from registers.  Data sorted by falling symbol frequency puts the
-    shortest codewords first, so its first tiles overflow (25.6 symbols per segment on
-    5-bit codewords); staging caps of 17 and 4 bytes per segment send about half / all
-    of a random stream's tiles through the direct path."""
+@pytest.mark.parametrize("r,scap", [(0.1, None), (0.1, "17"), (0.1, "4"), (0.5, None), (0.5, "22"), (0.5, "4")])
+def test_tile_staging_overflow(gpu, orc, r, scap, monkeypatch):
+    """The tile kernel's staging holds the typical tile, not the worst case 128 / minlen
+    bytes per segment (20 bytes per segment for r = 0.1 codes, the mean + 12 % for the
+    minlen-3 shape); a tile decoding to more bytes waits for its own prefix and stores
+    straight from registers.  Data sorted by falling symbol frequency puts the shortest
+    codewords first, so its first tiles overflow (25.6 symbols per segment on 5-bit
+    codewords, 42.7 on 3-bit ones); smaller staging caps send about half / all of a
+    random stream's tiles through the direct path."""
     monkeypatch.setenv("GH_MODE", "tile")
     if scap:
         monkeypatch.setenv("GH_TILE_SCAP", scap)
-    d = gpu.generate(31, 0.1, 3_000_001)
+    d = gpu.generate(31, r, 3_000_001)
     vals, cnts = np.unique(d, return_counts=True)
     rank = np.zeros(256, np.int64)
     rank[vals[np.argsort(-cnts, kind="stable")]] = np.arange(vals.size)
@@ -386,8 +390,8 @@ def test_tile_staging_overflow(gpu, orc, scap, monkeypatch):
         assert gpu.MODE_NAMES[rep.mode] == "tile" and rep.status == 0
 
 
-@pytest.mark.parametrize("mode", ["tile", "wsplit"])
-def test_decode_beside_a_foreign_kernel(gpu, mode, monkeypatch):
+@pytest.mark.parametrize("mode,r", [("tile", 0.1), ("tile", 0.5), ("wsplit", 0.5)])
+def test_decode_beside_a_foreign_kernel(gpu, mode, r, monkeypatch):
     """A persistent decode grid sized to the whole GPU, launched while another stream's
     kernel (a 1 GiB streaming copy, 131 K workgroups, repeated) holds the CUs: its
     workgroups become resident only as the copy's retire, and the ones already running
@@ -399,7 +403,6 @@ def test_decode_beside_a_foreign_kernel(gpu, mode, monkeypatch):
     import torch
 
     monkeypatch.setenv("GH_MODE", mode)
-    r = 0.5 if mode == "wsplit" else 0.1
     data = gpu.generate(91, r, 100_000_007)
     s = gpu.parse(gpu.encode(data))
     src = torch.full((1 << 30,), 7, dtype=torch.uint8, device="cuda")
