@@ -54,7 +54,10 @@ using namespace gh;
 // segments per lane with 8 output words each; codes with 3-bit codewords (at most 43
 // per segment, e.g. BASELINE's r = 0.5 codes) two segments per lane with 11 words (the
 // registers and the staging of a third segment would halve the workgroups per CU).
-constexpr uint32_t TILE_U3 = 2;  // segments per lane, minlen-3 codes
+#ifndef GH_TILE_U3
+#define GH_TILE_U3 2
+#endif
+constexpr uint32_t TILE_U3 = GH_TILE_U3;  // segments per lane, minlen-3 codes
 static uint32_t tile_u_for(uint32_t minlen) { return minlen >= 4 ? (uint32_t)TILE_U : TILE_U3; }
 static const void* tile_kernel_for(uint32_t minlen, uint32_t g) {
   if (minlen >= 4)
@@ -184,8 +187,10 @@ static int tile_setup(gh_ctx* c, uint32_t K, double avg_seg_bytes) {
   // workgroups fit a CU.  A tile is the sum of 1024-1536 segments, so it stays near its
   // mean; a larger one stores straight from registers (gh_tile_kernel).  GH_TILE_SCAP
   // overrides (tests).
+  double scapf = 1.12;
+  if (const char* e = getenv("GH_TILE_SCAPF")) scapf = std::clamp(atof(e), 0.5, 4.0);
   uint64_t per_seg = std::min<uint64_t>(
-      maxsyms, cn.minlen >= 4 ? (uint64_t)TILE_SCAP : (uint64_t)std::ceil(std::max(avg_seg_bytes, 1.0) * 1.12 + 1));
+      maxsyms, cn.minlen >= 4 ? (uint64_t)TILE_SCAP : (uint64_t)std::ceil(std::max(avg_seg_bytes, 1.0) * scapf + 1));
   if (const char* e = getenv("GH_TILE_SCAP")) per_seg = std::min<uint64_t>(maxsyms, (uint64_t)std::max(1, atoi(e)));
   c->stage_bytes = (uint32_t)((STAGE_PAD + (uint64_t)c->tile_u * TILE_TB * per_seg + 48 + 127) & ~127ull);
   const std::vector<uint32_t> lt = grouped_lut(cn, K);

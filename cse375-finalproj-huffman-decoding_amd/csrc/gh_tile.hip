@@ -63,6 +63,18 @@ constexpr int TILE_SCAP = 20;        // staging bytes per segment (larger tiles 
 #ifndef GH_TILE_NOZERO
 #define GH_TILE_NOZERO 1  // leave the decode's output words unzeroed (bytes past the count are never kept)
 #endif
+#ifndef GH_TILE_MERGEWAIT
+#define GH_TILE_MERGEWAIT 1
+#endif
+#ifndef GH_TILE_ABLATE
+#define GH_TILE_ABLATE 0  // diagnostic builds only (make variant): skip the decode
+#endif
+#ifndef GH_TILE_LDSPTR
+#define GH_TILE_LDSPTR 0  // LUT reads as plain LDS loads instead of inline ds_read + wait
+#endif
+#ifndef GH_TILE_ONEASM
+#define GH_TILE_ONEASM 0  // the chains' borrow counts in one asm block per lookup step
+#endif
 #ifndef GH_TILE_TRIM
 #define GH_TILE_TRIM 1  // stop shifting window words no kept codeword can still read
 #endif
@@ -129,6 +141,29 @@ __device__ __forceinline__ uint32_t q_init(bool act, int start) {
   return ((act ? (uint32_t)(127 - start) : 511u) << 23) | Q_SYMROOM | 32u;
 }
 
+// q[u] -= ent[u]; cnt[u] = pos1 where that borrows (the codeword that reaches the
+// segment end), for the U chains in one asm block.
+template <int U>
+__device__ __forceinline__ void borrow_count(uint32_t (&q)[U], uint32_t (&cnt)[U], const uint32_t (&ent)[U],
+                                             int pos1);
+template <>
+__device__ __forceinline__ void borrow_count<2>(uint32_t (&q)[2], uint32_t (&cnt)[2], const uint32_t (&ent)[2],
+                                                int pos1) {
+  asm("v_sub_co_u32 %0, vcc, %0, %4\n\tv_cndmask_b32_e64 %2, %2, %6, vcc\n\t"
+      "v_sub_co_u32 %1, vcc, %1, %5\n\tv_cndmask_b32_e64 %3, %3, %6, vcc"
+      : "+v"(q[0]), "+v"(q[1]), "+v"(cnt[0]), "+v"(cnt[1])
+      : "v"(ent[0]), "v"(ent[1]), "i"(pos1) : "vcc");
+}
+template <>
+__device__ __forceinline__ void borrow_count<3>(uint32_t (&q)[3], uint32_t (&cnt)[3], const uint32_t (&ent)[3],
+                                                int pos1) {
+  asm("v_sub_co_u32 %0, vcc, %0, %6\n\tv_cndmask_b32_e64 %3, %3, %9, vcc\n\t"
+      "v_sub_co_u32 %1, vcc, %1, %7\n\tv_cndmask_b32_e64 %4, %4, %9, vcc\n\t"
+      "v_sub_co_u32 %2, vcc, %2, %8\n\tv_cndmask_b32_e64 %5, %5, %9, vcc"
+      : "+v"(q[0]), "+v"(q[1]), "+v"(q[2]), "+v"(cnt[0]), "+v"(cnt[1]), "+v"(cnt[2])
+      : "v"(ent[0]), "v"(ent[1]), "v"(ent[2]), "i"(pos1) : "vcc");
+}
+
 // Decode of U segments per lane on e-windows, the U chains in lock-step (their LDS
 // reads are independent, so their latencies overlap).  Each group decodes G codewords
 // per chain from e0:e1 and then shifts the windows (G * maxlen <= 32, so the group's
@@ -167,16 +202,26 @@ __device__ __forceinline__ void decode_tile_grouped(uint32_t (&e)[U][5], const i
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const uint32_t x = j == 0 ? e[u][0] : __builtin_amdgcn_alignbit(e[u][0], e[u][1], q[u]);
-          ent[u] = lds_u32_nowait((x & amask) | laneoff);
+          if (GH_TILE_LDSPTR)  // a plain LDS load: the compiler counts lgkmcnt itself
+            ent[u] = *(const __attribute__((address_space(3))) uint32_t*)(
+                (const __attribute__((address_space(3))) uint8_t*)0 + ((x & amask) | laneoff));
+          else
+            ent[u] = lds_u32_nowait((x & amask) | laneoff);
         }
-        lds_wait(ent);
+        if (!GH_TILE_LDSPTR) lds_wait(ent);
+        if (GH_TILE_ONEASM) {
+          // the U borrow counts in one asm block: each inline asm boundary cost an s_nop
+          borrow_count<U>(q, cnt, ent, pos + 1);
+        } else {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          asm("v_sub_co_u32 %0, vcc, %0, %2\n\t"
-              "v_cndmask_b32_e64 %1, %1, %3, vcc"
-              : "+v"(q[u]), "+v"(cnt[u]) : "v"(ent[u]), "i"(pos + 1) : "vcc");
-          ow[u][pos >> 2] = __builtin_amdgcn_perm(ent[u], ow[u][pos >> 2], perm_sel(pos & 3));
+          for (int u = 0; u < U; ++u)
+            asm("v_sub_co_u32 %0, vcc, %0, %2\n\t"
+                "v_cndmask_b32_e64 %1, %1, %3, vcc"
+                : "+v"(q[u]), "+v"(cnt[u]) : "v"(ent[u]), "i"(pos + 1) : "vcc");
         }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          ow[u][pos >> 2] = __builtin_amdgcn_perm(ent[u], ow[u][pos >> 2], perm_sel(pos & 3));
       }
     }
     uint32_t qmin = 0xFFFFFFFFu;
@@ -469,7 +514,21 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE,
         start[u] = seg == 0 ? (int)p.first_start : (int)gap_nib(gw[u], p.gap_nib0 + seg - 1u);
         make_ewin(w[u], w4[u], start[u], S, e[u]);
       }
-      if (have_cur) {
+      // Decoded unconditionally: in the last iterations (no tile) every chain is inactive
+      // and the loop stops after one group (the loads were issued, clamped to the last
+      // tile).  A branch around the decode made the compiler zero the 24 output words
+      // before it every iteration, and merge at the scans a path on which the loads
+      // were not yet waited for: a vmcnt(0) after every decode, which also waited there
+      // for the mid-decode prefix load.  (GH_TILE_MERGEWAIT=0: the old branch.)
+      if (GH_TILE_ABLATE) {  // diagnostic build: no decode, 16 bytes per segment (wrong output)
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          cnt[u] = act[u] ? 16u : 0u;
+#pragma unroll
+          for (int k2 = 0; k2 < OW; ++k2) ow[u][k2] = e[u][k2 % 5];
+        }
+        mid();
+      } else if (GH_TILE_MERGEWAIT || have_cur) {
         decode_tile_grouped<GRP, U, OW, MINL, TILE_MIDG>(e, start, act, ow, cnt, amask, laneoff, mid);
       } else {
 #pragma unroll
@@ -495,8 +554,11 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE,
 #pragma unroll
     for (int u = 0; u < U; ++u) bpos[u] = incl[u] - cnt[u];
     // ---- copy tile k-2 out (its prefix was published about an iteration ago) ----------
+    // (one call site of load(nxt), after the prefix check: with a call in each branch the
+    // compiler hoisted the loads above the check, whose vmcnt(0) then waited for them)
+    unsigned long long goff = 0;
+    uint32_t n2 = 0;
     if (have2) {
-      unsigned long long goff = 0;
       bool polled = false, got = true;
       if (lane == 0) {
         polled = !granule_ok(p, gp, 2);
@@ -511,13 +573,12 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE,
       goff = rfl_u64(goff);
       ahead = __builtin_amdgcn_readfirstlane(polled ? 1 : 0) != 0;
       got = __builtin_amdgcn_readfirstlane(got ? 1 : 0) != 0;
-      const uint32_t n2 = (!got || goff >= p.out_cap) ? 0u : (uint32_t)min<unsigned long long>(tot2, p.out_cap - goff);
-      load(nxt);  // the next tile's words, issued before this copy-out's stores
+      n2 = (!got || goff >= p.out_cap) ? 0u : (uint32_t)min<unsigned long long>(tot2, p.out_cap - goff);
+    }
+    load(nxt);  // the next tile's words, issued before this copy-out's stores
+    if (have2)
       copy_out_tile<TB, TILE_NS>(p.out, p.lut_bytes + buf * p.stage_bytes, goff, n2, tid,
                                  p.junk + (unsigned long long)blockIdx.x * TB + tid);
-    } else {
-      load(nxt);
-    }
     __syncthreads();  // tile sums
     // the U x NWAVE_T wave sums in chain-then-wave order, one per lane, scanned with DPP:
     // wave w's chain-u segments start at the exclusive prefix of entry u * NWAVE_T + w
