@@ -192,6 +192,8 @@ static int tile_setup(gh_ctx* c, uint32_t K, double avg_seg_bytes) {
   uint64_t per_seg = std::min<uint64_t>(
       maxsyms, cn.minlen >= 4 ? (uint64_t)TILE_SCAP : (uint64_t)std::ceil(std::max(avg_seg_bytes, 1.0) * scapf + 1));
   if (const char* e = getenv("GH_TILE_SCAP")) per_seg = std::min<uint64_t>(maxsyms, (uint64_t)std::max(1, atoi(e)));
+  if (GH_TILE_NOTAIL)  // the copy-out's fixed TILE_NS stores per thread must cover a staged tile
+    per_seg = std::min<uint64_t>(per_seg, ((uint64_t)TILE_NS * TILE_TB * 16 - 256) / ((uint64_t)c->tile_u * TILE_TB));
   c->stage_bytes = (uint32_t)((STAGE_PAD + (uint64_t)c->tile_u * TILE_TB * per_seg + 48 + 127) & ~127ull);
   const std::vector<uint32_t> lt = grouped_lut(cn, K);
   const void* kern = tile_kernel_for(c->tile_minl, c->tile_g);
@@ -218,7 +220,7 @@ static int tile_setup(gh_ctx* c, uint32_t K, double avg_seg_bytes) {
   // occupancy; decodes on one device are chained, see DevChain)
   c->grid = (uint32_t)std::min<uint64_t>({(uint64_t)c->ntiles + 1, (uint64_t)best * c->num_cu, (uint64_t)LEAD_A * TILE_TB});
   if (c->grid < 2) return GH_OK;  // (the wave split then takes the code)
-  GH_HIP(hipMalloc(&c->d_tile_junk, 16ull * c->grid * TILE_TB));
+  GH_HIP(hipMalloc(&c->d_tile_junk, 16ull * c->grid * TILE_TB * (TILE_NS + 2)));
   c->tile = true;
   return GH_OK;
 }

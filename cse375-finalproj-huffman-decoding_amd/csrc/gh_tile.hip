@@ -39,6 +39,13 @@ constexpr int TILE_TB = 512;       // threads per workgroup
 #ifndef GH_TILE_U
 #define GH_TILE_U 3
 #endif
+#ifndef GH_TILE_NOTAIL
+#define GH_TILE_NOTAIL 0  // copy-out: NS = 4 fixed stores per thread, no loop for extra chunks
+#endif
+#if GH_TILE_NOTAIL
+#undef GH_TILE_NS
+#define GH_TILE_NS 4
+#endif
 #ifndef GH_TILE_NS
 #define GH_TILE_NS 2
 #endif
@@ -65,6 +72,9 @@ constexpr int TILE_SCAP = 20;        // staging bytes per segment (larger tiles 
 #endif
 #ifndef GH_TILE_MERGEWAIT
 #define GH_TILE_MERGEWAIT 1
+#endif
+#ifndef GH_TILE_EARLY
+#define GH_TILE_EARLY 0  // issue the next tile's loads before the decode instead of before the copy-out
 #endif
 #ifndef GH_TILE_ABLATE
 #define GH_TILE_ABLATE 0  // diagnostic builds only (make variant): skip the decode
@@ -98,7 +108,7 @@ struct TileParams {
   unsigned int gap_nib0, first_start, ntiles, kbits, lgr, epoch;
   unsigned int lut_bytes;        // LUT bytes in LDS (replicated: 4 << (K + lgr))
   unsigned int stage_bytes;      // one staging buffer
-  uint4* junk;                   // 16 bytes per thread of the grid for padding stores
+  uint4* junk;                   // padding stores: 16 bytes per thread of the grid, (TILE_NS + 2) slots
 };
 
 // LDS of the tile kernel: LUT, two staging buffers, wave sums, leader wave totals.
@@ -295,7 +305,7 @@ __device__ __forceinline__ void stage_head(uint32_t o, uint32_t h, uint32_t nb) 
 // no longer waits for its previous copy-out's stores to be acknowledged.  Chunks beyond
 // NS per thread (a tile larger than 16 * NS * TB bytes) loop.  stg: absolute LDS byte
 // address of the staging buffer.
-template <int TBK, int NS>
+template <int TBK, int NS, bool TAIL>
 __device__ __forceinline__ void copy_out_tile(uint8_t* out, uint32_t stg, unsigned long long goff, uint32_t n,
                                               int tid, uint4* junk) {
   const uint32_t lb = (uint32_t)(goff & 15);
@@ -304,16 +314,41 @@ __device__ __forceinline__ void copy_out_tile(uint8_t* out, uint32_t stg, unsign
   const uint32_t cf = lb ? 1u : 0u;        // interior chunks [cf, ce)
   const uint32_t ce = n ? (lb + n) >> 4 : 0u;
   const bool have = ce > cf;
+  if (TAIL) {
 #pragma unroll
-  for (int i = 0; i < NS; ++i) {
-    const uint32_t c = cf + (uint32_t)tid + (uint32_t)(TBK * i);
-    const bool real = c < ce;
-    const uint32_t cs = real ? c : ce - 1u;
-    const uint4 v = lds_u128(src + 16u * ((real || have) ? cs : cf));
-    *((real || have) ? (uint4*)(o + 16ull * cs) : junk) = v;
+    for (int i = 0; i < NS; ++i) {
+      const uint32_t c = cf + (uint32_t)tid + (uint32_t)(TBK * i);
+      const bool real = c < ce;
+      const uint32_t cs = real ? c : ce - 1u;
+      const uint4 v = lds_u128(src + 16u * ((real || have) ? cs : cf));
+      *((real || have) ? (uint4*)(o + 16ull * cs) : junk) = v;
+    }
+    for (uint32_t c = cf + (uint32_t)tid + (uint32_t)(TBK * NS); c < ce; c += TBK)
+      *(uint4*)(o + 16ull * c) = lds_u128(src + 16u * c);
+  } else {
+    // NS x TBK chunks cover every staged tile (the host sizes NS): no loop, so the
+    // store count is fixed and the next iteration's wait for its prefetched loads
+    // (issued before these stores) does not wait for these stores' acknowledgements.
+    // A store past the tile rewrites the thread's first chunk (same bytes, its own
+    // address: no two threads pad onto one line); no LDS read for it.
+    const uint32_t c0 = cf + (uint32_t)tid;
+    const bool real0 = c0 < ce;
+    const uint32_t cs0 = real0 ? c0 : (have ? ce - 1u : cf);
+    const uint4 v0 = lds_u128(src + 16u * cs0);
+    uint4* const d0 = (real0 || have) ? (uint4*)(o + 16ull * cs0) : junk;
+    *d0 = v0;
+#pragma unroll
+    for (int i = 1; i < NS; ++i) {
+      const uint32_t c = c0 + (uint32_t)(TBK * i);
+      uint4 v = v0;
+      uint4* d = d0;
+      if (c < ce) {
+        v = lds_u128(src + 16u * c);
+        d = (uint4*)(o + 16ull * c);
+      }
+      *d = v;
+    }
   }
-  for (uint32_t c = cf + (uint32_t)tid + (uint32_t)(TBK * NS); c < ce; c += TBK)
-    *(uint4*)(o + 16ull * c) = lds_u128(src + 16u * c);
   // edge bytes: the head chunk's [lb, min(16, lb + n)) when lb != 0, then the tail
   // chunk's [0, (lb + n) & 15) when it is another chunk; one byte per thread
   const uint32_t nh = (lb && n) ? min(16u, lb + n) - lb : 0u;
@@ -477,6 +512,13 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE,
     }
   };
   load(cur);
+  {  // as many stores after these loads as every iteration issues after its prefetch
+     // (the copy-out's TILE_NS + 1): the loop's entry then matches its back edge, and
+     // the compiler waits for the loads with a counted vmcnt instead of vmcnt(0)
+    const unsigned long long slot = (unsigned long long)blockIdx.x * TB + tid, nslot = (unsigned long long)gridDim.x * TB;
+#pragma unroll
+    for (int i = 0; i <= TILE_NS; ++i) p.junk[slot + (unsigned long long)(i + 1) * nslot] = make_uint4(0, 0, 0, 0);
+  }
   if (cur >= p.ntiles) cur = NONE;
   uint32_t t1 = NONE, t2 = NONE;  // tiles of iterations k-1, k-2
   uint32_t tot1 = 0, tot2 = 0;    // their totals
@@ -514,6 +556,10 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE,
         start[u] = seg == 0 ? (int)p.first_start : (int)gap_nib(gw[u], p.gap_nib0 + seg - 1u);
         make_ewin(w[u], w4[u], start[u], S, e[u]);
       }
+      // GH_TILE_EARLY: the next tile's loads right here, into the registers the windows
+      // were just built from, so they have the whole iteration to arrive (the prefix
+      // load issued mid-decode then waits behind them in the in-order vmcnt queue)
+      if (GH_TILE_EARLY) load(nxt);
       // Decoded unconditionally: in the last iterations (no tile) every chain is inactive
       // and the loop stops after one group (the loads were issued, clamped to the last
       // tile).  A branch around the decode made the compiler zero the 24 output words
@@ -575,10 +621,12 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE,
       got = __builtin_amdgcn_readfirstlane(got ? 1 : 0) != 0;
       n2 = (!got || goff >= p.out_cap) ? 0u : (uint32_t)min<unsigned long long>(tot2, p.out_cap - goff);
     }
-    load(nxt);  // the next tile's words, issued before this copy-out's stores
-    if (have2)
-      copy_out_tile<TB, TILE_NS>(p.out, p.lut_bytes + buf * p.stage_bytes, goff, n2, tid,
-                                 p.junk + (unsigned long long)blockIdx.x * TB + tid);
+    if (!GH_TILE_EARLY) load(nxt);  // the next tile's words, issued before this copy-out's stores
+    // Unconditional (no tile two iterations back: n2 = 0, every store goes to the thread's
+    // junk slot): the same store count on every path lets the compiler wait for the
+    // prefetched loads with a counted vmcnt at the top of the next iteration.
+    copy_out_tile<TB, TILE_NS, !GH_TILE_NOTAIL>(p.out, p.lut_bytes + buf * p.stage_bytes, goff, n2, tid,
+                                                 p.junk + (unsigned long long)blockIdx.x * TB + tid);
     __syncthreads();  // tile sums
     // the U x NWAVE_T wave sums in chain-then-wave order, one per lane, scanned with DPP:
     // wave w's chain-u segments start at the exclusive prefix of entry u * NWAVE_T + w
@@ -609,6 +657,9 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE,
 #pragma unroll
         for (int u = 0; u < U; ++u) store_direct(p.out, p.out_cap, goff + bpos[u], ow[u], cnt[u]);
       }
+      // (rare path) drain its data-dependent loads and stores here, so that the
+      // compiler's wait for the next tile's loads stays a counted vmcnt on the common path
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     } else if (have_cur) {
       // stage this tile into buffer k & 1 (copied out two iterations later) at its
       // absolute LDS address (the kernel's LDS starts at 0)
