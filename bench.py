@@ -69,6 +69,7 @@ KERNEL_NAMES = {
     (1, 3): "gh::gh_ms_count_kernel + gh::gh_ms_write_kernel",
     (1, -1): "gh::gh_count_kernel + gh::gh_write_kernel",
     (2, -1): "gh::gh_tile_kernel",
+    (3, -1): "gh::gh_ftile_kernel",
     (0, -1): "gh::gh_decode_kernel",
 }
 

@@ -54,7 +54,10 @@ constexpr int TILE_TB = 512;       // threads per workgroup
 #endif
 constexpr int TILE_U = GH_TILE_U;    // segments per lane
 constexpr int TILE_NS = GH_TILE_NS;  // 16-byte stores per thread per copy-out (the rest of a tile loops)
-constexpr int TILE_SCAP = 20;        // staging bytes per segment (larger tiles bypass staging)
+#ifndef GH_TILE_SCAPB
+#define GH_TILE_SCAPB 20
+#endif
+constexpr int TILE_SCAP = GH_TILE_SCAPB;  // staging bytes per segment (larger tiles bypass staging)
 #ifndef GH_TILE_MIDG
 #define GH_TILE_MIDG 2
 #endif
@@ -76,8 +79,32 @@ constexpr int TILE_SCAP = 20;        // staging bytes per segment (larger tiles 
 #ifndef GH_TILE_EARLY
 #define GH_TILE_EARLY 0  // issue the next tile's loads before the decode instead of before the copy-out
 #endif
+#ifndef GH_TILE_BATCH
+#define GH_TILE_BATCH 0  // copy-out: the thread's LDS reads issued together behind one wait
+#endif
+#ifndef GH_TILE_WPRIO
+#define GH_TILE_WPRIO 0  // waves 4-7 (the second wave on each SIMD) one issue priority level up
+#endif
+#ifndef GH_TILE_P1MIN
+#define GH_TILE_P1MIN 0  // staging phase 1: the first dwords every kept segment fills, unmasked
+#endif
+#ifndef GH_TILE_IOVL
+#define GH_TILE_IOVL 0  // copy-out parts between the decode groups of the next tile
+#endif
+#ifndef GH_TILE_IOB
+#define GH_TILE_IOB 2   // (IOVL) the decode group after which the prefix is checked
+#endif
+#ifndef GH_TILE_STAMPS
+#define GH_TILE_STAMPS 0  // diagnostic builds only: per-phase s_memtime deltas of waves 0 and 4
+#endif
+#if GH_TILE_STAMPS
+#define TSTAMP(i) (ts[i] = __builtin_amdgcn_s_memtime())
+#else
+#define TSTAMP(i) ((void)0)
+#endif
 #ifndef GH_TILE_ABLATE
-#define GH_TILE_ABLATE 0  // diagnostic builds only (make variant): skip the decode
+#define GH_TILE_ABLATE 0  // diagnostic builds only (make variant), bits: 1 no decode, 2 no staging
+                          // stores, 4 no prefix wait (a fake offset), 8 no copy-out (wrong output)
 #endif
 #ifndef GH_TILE_LDSPTR
 #define GH_TILE_LDSPTR 0  // LUT reads as plain LDS loads instead of inline ds_read + wait
@@ -109,6 +136,12 @@ struct TileParams {
   unsigned int lut_bytes;        // LUT bytes in LDS (replicated: 4 << (K + lgr))
   unsigned int stage_bytes;      // one staging buffer
   uint4* junk;                   // padding stores: 16 bytes per thread of the grid, (TILE_NS + 2) slots
+  uint4* stamps;                 // GH_TILE_STAMPS builds: [grid][2 waves][128 iterations][2] phase deltas
+  // fused count + write tile kernel (gh_ftile.hip): lut = count LUT (Kc = kbits, at LDS 0)
+  const uint2* lutw;             // write LUT (2^kw u64 entries {symbols, b | n << 8})
+  unsigned int kw, lutw_off, lutw_bytes;  // its width, LDS offset (a multiple of 8 << kw), bytes
+  unsigned int stage_off;        // LDS offset of the staging
+  unsigned int last_end;         // end bit of the stream's last segment when the shard holds it (else 0)
 };
 
 // LDS of the tile kernel: LUT, two staging buffers, wave sums, leader wave totals.
@@ -180,11 +213,11 @@ __device__ __forceinline__ void borrow_count<3>(uint32_t (&q)[3], uint32_t (&cnt
 // consumed bits fit Q's low byte).  Codeword j of a segment goes to byte j of ow (v_perm,
 // static index); dead codewords go there too and are never staged.  `mid()` runs once,
 // after group MIDG (or at the end if the loop stops earlier).
-template <int G, int U, int OW, int MINL, int MIDG, class Mid>
+template <int G, int U, int OW, int MINL, class Hook, class Finish>
 __device__ __forceinline__ void decode_tile_grouped(uint32_t (&e)[U][5], const int (&start)[U],
                                                     const bool (&act)[U], uint32_t (&ow)[U][OW],
                                                     uint32_t (&cnt)[U], uint32_t amask, uint32_t laneoff,
-                                                    Mid&& mid) {
+                                                    Hook&& hook, Finish&& finish) {
   constexpr int S = 4 * OW;
   constexpr int NG = (S + G - 1) / G;
   uint32_t q[U];
@@ -201,7 +234,7 @@ __device__ __forceinline__ void decode_tile_grouped(uint32_t (&e)[U][5], const i
       else ow[u][k] = 0;
     }
   }
-  bool mid_done = false;
+  int gdone = NG;  // groups run (the loop stops once no chain is live)
 #pragma unroll
   for (int gi = 0; gi < NG; ++gi) {
 #pragma unroll
@@ -252,13 +285,13 @@ __device__ __forceinline__ void decode_tile_grouped(uint32_t (&e)[U][5], const i
       q[u] = (q[u] & 0xFFFFFF00u) | 32u;
       qmin = min(qmin, q[u]);
     }
-    if (gi == MIDG) {
-      mid();
-      mid_done = true;
+    hook(gi);  // a constant in the unrolled loop
+    if (gi + 1 < NG && !__any(qmin < Q_LIVE)) {
+      gdone = gi + 1;
+      break;
     }
-    if (gi + 1 < NG && !__any(qmin < Q_LIVE)) break;
   }
-  if (!mid_done) mid();
+  finish(gdone);
 }
 
 __device__ __forceinline__ void lds_st32(uint32_t a, uint32_t v) {
@@ -272,7 +305,7 @@ __device__ __forceinline__ void lds_st32(uint32_t a, uint32_t v) {
 // skipped first dword) exactly, over the previous segment's phase-1 tail.  Every dword
 // store is aligned: unaligned ds_write_b32 measured about 3x the LDS time of aligned
 // ones with per-lane offsets like these.  Returns the number of head bytes.
-template <int OW>
+template <int OW, int MINW = 0>
 __device__ __forceinline__ uint32_t stage_aligned_p1(const uint32_t (&ow)[OW], uint32_t n, uint32_t o) {
   const uint32_t ap = ((o - 1u) & 3u) + 1u;  // 1..4: bytes from the dword base to o
   const uint32_t base = o - ap;              // dword m at base + 4m holds segment bytes [4m - ap, +4)
@@ -282,7 +315,9 @@ __device__ __forceinline__ uint32_t stage_aligned_p1(const uint32_t (&ow)[OW], u
   for (int m = 1; m <= OW; ++m) {
     const uint32_t hi = m < OW ? ow[m] : 0u;
     const uint32_t r = __builtin_amdgcn_alignbyte(hi, ow[m - 1], s);
-    if ((uint32_t)m <= last) lds_st32(base + 4u * m, r);
+    // dwords 1..MINW are touched by every segment of >= 4 * MINW codewords (the caller
+    // guarantees it for every kept segment): stored without a per-lane test
+    if (m <= MINW || (uint32_t)m <= last) lds_st32(base + 4u * m, r);
   }
   return min(4u - ap, n);  // (n >= 4 - ap for every grouped code; never write past n)
 }
@@ -314,6 +349,47 @@ __device__ __forceinline__ void copy_out_tile(uint8_t* out, uint32_t stg, unsign
   const uint32_t cf = lb ? 1u : 0u;        // interior chunks [cf, ce)
   const uint32_t ce = n ? (lb + n) >> 4 : 0u;
   const bool have = ce > cf;
+  if constexpr (TAIL && GH_TILE_BATCH) {
+    // every read of this thread's chunks and edge byte issued, then one wait, then the
+    // stores (one LDS round trip instead of one per chunk)
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    v4u v[NS];
+    uint32_t cs[NS];
+    v4u* d[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      const uint32_t c = cf + (uint32_t)tid + (uint32_t)(TBK * i);
+      const bool real = c < ce;
+      cs[i] = real ? c : ce - 1u;
+      asm volatile("ds_read_b128 %0, %1" : "=v"(v[i]) : "v"(src + 16u * ((real || have) ? cs[i] : cf)) : "memory");
+      d[i] = (real || have) ? (v4u*)(o + 16ull * cs[i]) : (v4u*)junk;
+    }
+    const uint32_t nh = (lb && n) ? min(16u, lb + n) - lb : 0u;
+    const uint32_t tl = (lb + n) & 15u;
+    const uint32_t nt = (n && tl && (ce > 0 || !lb)) ? tl : 0u;
+    const uint32_t t = (uint32_t)tid;
+    const bool hb = nh + nt > 0;
+    uint32_t k = nh ? lb : 16u * ce;
+    bool real = false;
+    if (t < nh) {
+      k = lb + t;
+      real = true;
+    } else if (t < nh + nt) {
+      k = 16u * ce + (t - nh);
+      real = true;
+    }
+    uint32_t b;
+    asm volatile("ds_read_u8 %0, %1" : "=v"(b) : "v"(src + ((real || hb) ? k : 0u)) : "memory");
+    static_assert(NS == 2 || NS == 3, "batched copy-out: 2 or 3 chunks per thread");
+    if constexpr (NS == 2) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(b)::"memory");
+    else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(b)::"memory");
+#pragma unroll
+    for (int i = 0; i < NS; ++i) *d[i] = v[i];
+    *((real || hb) ? o + k : (uint8_t*)junk) = (uint8_t)b;
+    for (uint32_t c = cf + (uint32_t)tid + (uint32_t)(TBK * NS); c < ce; c += TBK)
+      *(uint4*)(o + 16ull * c) = lds_u128(src + 16u * c);
+    return;
+  }
   if (TAIL) {
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
@@ -369,6 +445,55 @@ __device__ __forceinline__ void copy_out_tile(uint8_t* out, uint32_t stg, unsign
   asm volatile("ds_read_u8 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(b) : "v"(src + ((real || hb) ? k : 0u)) : "memory");
   *((real || hb) ? o + k : (uint8_t*)junk) = (uint8_t)b;
 }
+
+// The copy-out of copy_out_tile<TBK, NS, true> cut into parts (GH_TILE_IOVL): chunk i
+// of every thread, then the edge byte, then the loop over chunks beyond NS per thread,
+// so that the parts can run between the decode groups of the next tile.
+template <int TBK, int NS>
+struct CopyParts {
+  uint8_t* o = nullptr;
+  uint32_t src = 0, cf = 0, ce = 0, lb = 0, n = 0;
+  bool have = false;
+  __device__ __forceinline__ void init(uint8_t* out, uint32_t stg, unsigned long long goff, uint32_t n_) {
+    n = n_;
+    lb = (uint32_t)(goff & 15);
+    o = out + (goff - lb);
+    src = stg + 16u - lb;
+    cf = lb ? 1u : 0u;
+    ce = n ? (lb + n) >> 4 : 0u;
+    have = ce > cf;
+  }
+  __device__ __forceinline__ void chunk(int i, int tid, uint4* junk) const {
+    const uint32_t c = cf + (uint32_t)tid + (uint32_t)(TBK * i);
+    const bool real = c < ce;
+    const uint32_t cs = real ? c : ce - 1u;
+    const uint4 v = lds_u128(src + 16u * ((real || have) ? cs : cf));
+    *((real || have) ? (uint4*)(o + 16ull * cs) : junk) = v;
+  }
+  __device__ __forceinline__ void edge(int tid, uint4* junk) const {
+    const uint32_t nh = (lb && n) ? min(16u, lb + n) - lb : 0u;
+    const uint32_t tl = (lb + n) & 15u;
+    const uint32_t nt = (n && tl && (ce > 0 || !lb)) ? tl : 0u;
+    const uint32_t t = (uint32_t)tid;
+    const bool hb = nh + nt > 0;
+    uint32_t k = nh ? lb : 16u * ce;
+    bool real = false;
+    if (t < nh) {
+      k = lb + t;
+      real = true;
+    } else if (t < nh + nt) {
+      k = 16u * ce + (t - nh);
+      real = true;
+    }
+    uint32_t b;
+    asm volatile("ds_read_u8 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(b) : "v"(src + ((real || hb) ? k : 0u)) : "memory");
+    *((real || hb) ? o + k : (uint8_t*)junk) = (uint8_t)b;
+  }
+  __device__ __forceinline__ void tail(int tid) const {
+    for (uint32_t c = cf + (uint32_t)tid + (uint32_t)(TBK * NS); c < ce; c += TBK)
+      *(uint4*)(o + 16ull * c) = lds_u128(src + 16u * c);
+  }
+};
 
 // A segment's n bytes (ow, byte 0 first) stored to out[o, o + n), clamped at cap: the
 // path of a tile too large for staging (byte stores; rare).
@@ -524,7 +649,12 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE,
   uint32_t tot1 = 0, tot2 = 0;    // their totals
   uint32_t buf = 0;               // k & 1
   bool ahead = false;             // the last prefix had to be polled
+  unsigned long long gpc = 0;     // (IOVL) prefix of the next iteration's tile k-2, loaded early
+#if GH_TILE_STAMPS
+  unsigned long long ts[9];
+#endif
   for (uint32_t k = 0;; ++k) {
+    TSTAMP(0);
     const bool have_cur = cur < p.ntiles;
     const bool have2 = t2 < p.ntiles;  // tile k-2 is copied out this iteration
     if (!have_cur && t1 >= p.ntiles && !have2) break;
@@ -533,14 +663,80 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE,
       break;
     }
     const uint32_t par = k & 1u;
-    if (ahead) __builtin_amdgcn_s_setprio(GH_TILE_PLO);
-    else __builtin_amdgcn_s_setprio(GH_TILE_PHI);
+    if (GH_TILE_WPRIO && wid >= 4) {
+      if (ahead) __builtin_amdgcn_s_setprio(GH_TILE_PLO + 1);
+      else __builtin_amdgcn_s_setprio(GH_TILE_PHI + 1);
+    } else {
+      if (ahead) __builtin_amdgcn_s_setprio(GH_TILE_PLO);
+      else __builtin_amdgcn_s_setprio(GH_TILE_PHI);
+    }
     // prefix of tile k-2 (lane 0 of every wave): loaded mid-decode (a load issued at the
     // top often saw the value a little before it was published, and the re-poll then
     // paid a full memory round trip)
-    unsigned long long gp = 0;
+    unsigned long long gp = GH_TILE_IOVL ? gpc : 0ull;
     auto mid = [&]() {
-      if (have2 && lane == 0) gp = __hip_atomic_load(&p.prefix[t2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (!GH_TILE_IOVL && have2 && lane == 0 && !(GH_TILE_ABLATE & 4))
+        gp = __hip_atomic_load(&p.prefix[t2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    // ---- the prefix of tile k-2 -> its output offset (lane 0 of every wave) -----------
+    unsigned long long goff = 0;
+    uint32_t n2 = 0;
+    auto prefix_check = [&]() {
+      if (have2 && (GH_TILE_ABLATE & 4)) {
+        goff = ((unsigned long long)t2 * (U * TB * 16)) % (p.out_cap - (U * TB * 32));
+        n2 = tot2;
+      } else if (have2) {
+        bool polled = false, got = true;
+        if (lane == 0) {
+          polled = !granule_ok(p, gp, 2);
+          if (polled) {
+            if (wid == 0) atomicAdd(p.stats, 1ull);
+            gp = poll_granule(p, &p.prefix[t2], 2);
+            got = granule_ok(p, gp, 2);  // false only after a timeout (then nothing is written)
+          }
+          goff = gp & GRAN_VMASK;
+          if (wid == 0 && t2 == p.ntiles - 1 && got) *p.total = goff + tot2;
+        }
+        goff = rfl_u64(goff);
+        ahead = __builtin_amdgcn_readfirstlane(polled ? 1 : 0) != 0;
+        got = __builtin_amdgcn_readfirstlane(got ? 1 : 0) != 0;
+        n2 = (!got || goff >= p.out_cap) ? 0u : (uint32_t)min<unsigned long long>(tot2, p.out_cap - goff);
+      }
+    };
+    // (IOVL) the copy-out of tile k-2 in parts after decode groups IOB .. IOB + NS
+    CopyParts<TB, TILE_NS> co;
+    uint4* const jk = p.junk + (unsigned long long)blockIdx.x * TB + tid;
+    auto co_part = [&](int j) {
+      if (j == 0) {
+        prefix_check();
+        co.init(p.out, p.lut_bytes + buf * p.stage_bytes, goff, n2);
+      }
+      if (j < TILE_NS) co.chunk(j, tid, jk);
+      else co.edge(tid, jk);
+    };
+    auto hook = [&](int gi) {
+      if (GH_TILE_IOVL) {
+        if (gi >= GH_TILE_IOB && gi <= GH_TILE_IOB + TILE_NS) co_part(gi - GH_TILE_IOB);
+      } else if (gi == TILE_MIDG) {
+        mid();
+      }
+    };
+    auto finish = [&](int gdone) {
+      if (GH_TILE_IOVL) {
+#pragma unroll
+        for (int j = 0; j <= TILE_NS; ++j)
+          if (gdone <= GH_TILE_IOB + j) co_part(j);
+        co.tail(tid);
+        // then the prefix of tile k-1 (the next iteration's copy-out; published about
+        // an iteration ago) and the next tile's words, in that order: the copy-out's
+        // stores are older than both, and the top of the next iteration waits only for
+        // the loads (the stores, issued during the decode, have long completed)
+        if (lane == 0 && t1 < p.ntiles && !(GH_TILE_ABLATE & 4))
+          gpc = __hip_atomic_load(&p.prefix[t1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        load(nxt);
+      } else if (gdone <= TILE_MIDG) {
+        mid();
+      }
     };
     // ---- decode this tile (its words were loaded during the previous iteration) --------
     const uint32_t seg0 = cur * (uint32_t)(U * TB) + (uint32_t)tid;
@@ -556,6 +752,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE,
         start[u] = seg == 0 ? (int)p.first_start : (int)gap_nib(gw[u], p.gap_nib0 + seg - 1u);
         make_ewin(w[u], w4[u], start[u], S, e[u]);
       }
+      TSTAMP(1);
       // GH_TILE_EARLY: the next tile's loads right here, into the registers the windows
       // were just built from, so they have the whole iteration to arrive (the prefix
       // load issued mid-decode then waits behind them in the in-order vmcnt queue)
@@ -566,16 +763,16 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE,
       // before it every iteration, and merge at the scans a path on which the loads
       // were not yet waited for: a vmcnt(0) after every decode, which also waited there
       // for the mid-decode prefix load.  (GH_TILE_MERGEWAIT=0: the old branch.)
-      if (GH_TILE_ABLATE) {  // diagnostic build: no decode, 16 bytes per segment (wrong output)
+      if (GH_TILE_ABLATE & 1) {  // diagnostic build: no decode, 16 bytes per segment (wrong output)
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           cnt[u] = act[u] ? 16u : 0u;
 #pragma unroll
           for (int k2 = 0; k2 < OW; ++k2) ow[u][k2] = e[u][k2 % 5];
         }
-        mid();
+        finish(0);
       } else if (GH_TILE_MERGEWAIT || have_cur) {
-        decode_tile_grouped<GRP, U, OW, MINL, TILE_MIDG>(e, start, act, ow, cnt, amask, laneoff, mid);
+        decode_tile_grouped<GRP, U, OW, MINL>(e, start, act, ow, cnt, amask, laneoff, hook, finish);
       } else {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -583,13 +780,14 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE,
 #pragma unroll
           for (int k2 = 0; k2 < OW; ++k2) ow[u][k2] = 0;
         }
-        mid();
+        finish(0);
       }
     }
     // wave scans of the counts, before the copy-out: placed after it, the compiler waited
     // for every outstanding load and store (vmcnt(0)) in the middle of the scans
     // (the U scans are independent: issued together, their DPP steps interleave without
     // the wait states one scan alone needs; then one exec-masked block for the stores)
+    TSTAMP(2);
     uint32_t bpos[U], incl[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) incl[u] = wave_incl_scan(cnt[u]);
@@ -599,35 +797,22 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE,
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) bpos[u] = incl[u] - cnt[u];
+    TSTAMP(3);
     // ---- copy tile k-2 out (its prefix was published about an iteration ago) ----------
     // (one call site of load(nxt), after the prefix check: with a call in each branch the
     // compiler hoisted the loads above the check, whose vmcnt(0) then waited for them)
-    unsigned long long goff = 0;
-    uint32_t n2 = 0;
-    if (have2) {
-      bool polled = false, got = true;
-      if (lane == 0) {
-        polled = !granule_ok(p, gp, 2);
-        if (polled) {
-          if (wid == 0) atomicAdd(p.stats, 1ull);
-          gp = poll_granule(p, &p.prefix[t2], 2);
-          got = granule_ok(p, gp, 2);  // false only after a timeout (then nothing is written)
-        }
-        goff = gp & GRAN_VMASK;
-        if (wid == 0 && t2 == p.ntiles - 1 && got) *p.total = goff + tot2;
-      }
-      goff = rfl_u64(goff);
-      ahead = __builtin_amdgcn_readfirstlane(polled ? 1 : 0) != 0;
-      got = __builtin_amdgcn_readfirstlane(got ? 1 : 0) != 0;
-      n2 = (!got || goff >= p.out_cap) ? 0u : (uint32_t)min<unsigned long long>(tot2, p.out_cap - goff);
-    }
-    if (!GH_TILE_EARLY) load(nxt);  // the next tile's words, issued before this copy-out's stores
+    if (!GH_TILE_IOVL) prefix_check();
+    TSTAMP(4);
+    if (!GH_TILE_EARLY && !GH_TILE_IOVL) load(nxt);  // the next tile's words, issued before this copy-out's stores
     // Unconditional (no tile two iterations back: n2 = 0, every store goes to the thread's
     // junk slot): the same store count on every path lets the compiler wait for the
     // prefetched loads with a counted vmcnt at the top of the next iteration.
-    copy_out_tile<TB, TILE_NS, !GH_TILE_NOTAIL>(p.out, p.lut_bytes + buf * p.stage_bytes, goff, n2, tid,
-                                                 p.junk + (unsigned long long)blockIdx.x * TB + tid);
+    if (!(GH_TILE_ABLATE & 8) && !GH_TILE_IOVL)
+      copy_out_tile<TB, TILE_NS, !GH_TILE_NOTAIL>(p.out, p.lut_bytes + buf * p.stage_bytes, goff, n2, tid,
+                                                   p.junk + (unsigned long long)blockIdx.x * TB + tid);
+    TSTAMP(5);
     __syncthreads();  // tile sums
+    TSTAMP(6);
     // the U x NWAVE_T wave sums in chain-then-wave order, one per lane, scanned with DPP:
     // wave w's chain-u segments start at the exclusive prefix of entry u * NWAVE_T + w
     static_assert(U * NWAVE_T <= 64, "one wave sum per lane");
@@ -670,13 +855,29 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE,
         nb[u] = 0;
         hv[u] = ow[u][0];
         ha[u] = sbase + bpos[u];
-        if (cnt[u]) nb[u] = stage_aligned_p1(ow[u], cnt[u], ha[u]);
+        // a kept segment spans >= 113 bits, so it holds >= ceil(113 / maxlen) codewords
+        // (>= 12 when GRP >= 3, >= 10 otherwise; the stream's last segment may hold fewer,
+        // and its extra dwords land in the staging margin behind the tile)
+        constexpr int MINW = GH_TILE_P1MIN ? (GRP >= 3 ? 3 : 2) : 0;
+        if (cnt[u] && !(GH_TILE_ABLATE & 2)) nb[u] = stage_aligned_p1<OW, MINW>(ow[u], cnt[u], ha[u]);
       }
+      TSTAMP(7);
       __syncthreads();  // phase 1 done: every segment's tail dword is in place
 #pragma unroll
       for (int u = 0; u < U; ++u)
         if (nb[u]) stage_head(ha[u], hv[u], nb[u]);
     }
+#if GH_TILE_STAMPS
+    TSTAMP(8);
+    if (!(have_cur && staged)) ts[7] = ts[8];
+    if (lane == 0 && (wid & 3) == 0 && k < 128) {
+      uint4* st = p.stamps + (((unsigned long long)blockIdx.x * 2 + (wid >> 2)) * 128 + k) * 2;
+      st[0] = make_uint4((uint32_t)(ts[1] - ts[0]), (uint32_t)(ts[2] - ts[1]), (uint32_t)(ts[3] - ts[2]),
+                         (uint32_t)(ts[4] - ts[3]));
+      st[1] = make_uint4((uint32_t)(ts[5] - ts[4]), (uint32_t)(ts[6] - ts[5]), (uint32_t)(ts[7] - ts[6]),
+                         (uint32_t)(ts[8] - ts[7]));
+    }
+#endif
     t2 = t1;
     tot2 = tot1;
     t1 = staged ? cur : NONE;

@@ -105,7 +105,7 @@ class gh_sync_report(ctypes.Structure):
                 ("kernel_ms", ctypes.c_float)]
 
 
-MODE_NAMES = {1: "split", 2: "tile"}
+MODE_NAMES = {1: "split", 2: "tile", 3: "fused"}
 PATH_NAMES = {2: "grouped", 4: "multi_wave"}
 
 

@@ -1,0 +1,35 @@
+# Per-phase timing of the tile kernel from a GH_TILE_STAMPS build (make variant V=st
+# VFLAGS=-DGH_TILE_STAMPS=1): decodes a workload with that library, reads the last
+# decode's s_memtime deltas (waves 0 and 4 of every workgroup, first 128 iterations)
+# and prints the mean cycles per phase, by workgroup half (dispatch slot) and wave.
+# Usage: python scripts/stamps.py [name:N:r] [lib-suffix]
+import os, subprocess, sys, tempfile
+import numpy as np
+
+here = os.path.dirname(os.path.abspath(__file__))
+wl = sys.argv[1] if len(sys.argv) > 1 else "cfg4:1000000000:0.1"
+suffix = sys.argv[2] if len(sys.argv) > 2 else "st"
+out = os.path.join(tempfile.gettempdir(), f"gh_stamps_{os.getpid()}.bin")
+lib = os.path.join(here, "..", "cse375-finalproj-huffman-decoding_amd", "lib", f"libgaphuff_{suffix}.so")
+env = dict(os.environ, GAPHUFF_LIB=lib, GH_STAMPS_OUT=out)
+r = subprocess.run([sys.executable, os.path.join(here, "quick_one.py"), wl, "3"], env=env, capture_output=True,
+                   text=True, timeout=300)
+print(r.stdout.strip(), r.stderr.strip()[-500:])
+a = np.fromfile(out, dtype=np.uint32)
+os.unlink(out)
+grid = a.size // (2 * 128 * 8)
+a = a.reshape(grid, 2, 128, 8).astype(np.float64)
+names = ["load wait", "decode", "scans", "prefix", "copy-out", "barrier 1", "publish+stage1", "barrier 2+stage2"]
+valid = a.sum(axis=3) > 0
+valid[0] = False  # workgroup 0 leads the rounds
+print(f"grid {grid}, stamped iterations {int(valid.sum())}")
+for label, sel in [("all", np.ones(grid, bool)), ("WG < grid/2", np.arange(grid) < grid // 2),
+                   ("WG >= grid/2", np.arange(grid) >= grid // 2)]:
+    for wv in (0, 1):
+        m = valid[:, wv, :] & sel[:, None]
+        d = a[:, wv, :, :][m]
+        if d.size == 0:
+            continue
+        tot = d.sum(axis=1).mean()
+        parts = "  ".join(f"{n} {d[:, i].mean():7.0f}" for i, n in enumerate(names))
+        print(f"{label:13s} wave {4 * wv}: total {tot:7.0f} | {parts}")

@@ -1,0 +1,152 @@
+"""GPU parity tests of the fused count + write tile kernel (gh_ftile.hip, GH_MODE=fused):
+the wave split's codes without its fallback (BASELINE's r = 0.9 and r = 0.5 codes,
+complete, codewords up to the tables' widths) decoded by one persistent kernel that
+reads the payload once.  Bit-exact against the CPU oracle and the original input
+(reference: decoder/src/decoder.cu:454-730, restated in oracle/gh_oracle.c)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(gpu, orc, data, **kw):
+    img = gpu.encode(data)
+    out = gpu.decode(img, **kw)
+    ref, _ = orc.decode(img)
+    assert np.array_equal(ref, np.asarray(data, dtype=np.uint8))
+    if not np.array_equal(out, ref):
+        bad = np.nonzero(out != ref)[0]
+        raise AssertionError(f"{bad.size} mismatches, first at {bad[0]} of {out.size}")
+    return img
+
+
+def _report(gpu, img):
+    with gpu.Decoder(0) as d:
+        d.load(gpu.parse(img))
+        d.decode()
+        return d.report()
+
+
+@pytest.fixture
+def fused(monkeypatch):
+    monkeypatch.setenv("GH_MODE", "fused")
+
+
+@pytest.mark.parametrize("r", [0.5, 0.9, 0.999])
+@pytest.mark.parametrize("n", [1, 2, 7, 100, 4097, 65549, 1_000_003, 5_000_011])
+def test_fused_vs_oracle(gpu, orc, fused, r, n):
+    img = _check(gpu, orc, gpu.generate(2000 + n, r, n))
+    rep = _report(gpu, img)
+    assert gpu.MODE_NAMES[rep.mode] == "fused" and rep.status == 0
+
+
+def test_fused_small_codes(gpu, orc, fused):
+    # one-bit codes (two symbols: 128 codewords per segment), 8-bit codes, and a
+    # segment-multiple stream
+    rng = np.random.default_rng(3)
+    _check(gpu, orc, (rng.integers(0, 2, 300_001) + 48).astype(np.uint8))
+    data = np.tile(np.arange(256, dtype=np.uint8), 64)
+    rng.shuffle(data)
+    _check(gpu, orc, data)
+
+
+def test_fused_refuses_fallback_codes(gpu, fused):
+    """Codes longer than the tables (16-bit codewords) need the wave split's canonical
+    fallback: GH_MODE=fused fails loudly at load."""
+    counts = [max(1, int(2 ** (24 - 0.9 * i))) for i in range(40)]
+    data = np.repeat(np.arange(40, dtype=np.uint8), counts)
+    s = gpu.parse(gpu.encode(data))
+    with gpu.Decoder(0) as d:
+        with pytest.raises(gpu.GapHuffError):
+            d.load(s)
+
+
+@pytest.mark.parametrize("r,scap", [(0.9, None), (0.9, "30"), (0.9, "4"), (0.5, None), (0.5, "4")])
+def test_fused_staging_overflow(gpu, orc, fused, r, scap, monkeypatch):
+    """Staging holds the mean tile + 5 %; a tile decoding to more bytes waits for its
+    own prefix and stores straight to the output.  Data sorted by falling frequency puts
+    the shortest codewords first (its first tiles overflow); smaller staging caps send
+    about half / all of a random stream's tiles through the direct path."""
+    if scap:
+        monkeypatch.setenv("GH_TILE_SCAP", scap)
+    d = gpu.generate(31, r, 3_000_001)
+    vals, cnts = np.unique(d, return_counts=True)
+    rank = np.zeros(256, np.int64)
+    rank[vals[np.argsort(-cnts, kind="stable")]] = np.arange(vals.size)
+    dense = d[np.argsort(rank[d], kind="stable")]
+    for x in (dense, d):
+        img = _check(gpu, orc, x)
+        rep = _report(gpu, img)
+        assert gpu.MODE_NAMES[rep.mode] == "fused" and rep.status == 0
+
+
+@pytest.mark.parametrize("r,scap", [(0.9, None), (0.9, "4"), (0.5, None)])
+def test_fused_output_capacity_below_total(gpu, fused, r, scap, monkeypatch):
+    if scap:
+        monkeypatch.setenv("GH_TILE_SCAP", scap)
+    data = gpu.generate(81, r, 2_000_003)
+    s = gpu.parse(gpu.encode(data))
+    for cap in (1, 9, 16, 4099, 777_777, 1_999_990):
+        with gpu.Decoder(0) as d:
+            d.load(s, 0, s.g, out_cap=cap)
+            d.decode()
+            rep = d.report()
+            assert rep.status == 0 and rep.out_bytes == cap
+            got = d.download(cap)
+            if not np.array_equal(got, data[:cap]):
+                bad = np.nonzero(got != data[:cap])[0]
+                raise AssertionError(f"cap={cap}: {bad.size} wrong bytes, first at {bad[0]}")
+
+
+@pytest.mark.parametrize("nshards", [2, 3, 8])
+def test_fused_shards(gpu, orc, fused, nshards):
+    _check(gpu, orc, gpu.generate(11, 0.9, 2_000_000), ngpus=nshards, devices=[0] * nshards)
+
+
+def test_fused_shard_counts(gpu, orc, fused):
+    data = gpu.generate(12, 0.9, 300_000)
+    img = gpu.encode(data)
+    s = gpu.parse(img)
+    bounds = gpu.plan_shards(s.g, 5)
+    off = 0
+    for k in range(5):
+        with gpu.Decoder(0) as d:
+            d.load(s, bounds[k], bounds[k + 1])
+            d.decode()
+            r = d.report()
+            assert r.symbols == sum(orc.segment_count(img, i) for i in range(bounds[k], bounds[k + 1]))
+            keep = min(r.symbols, s.n - off)
+            assert np.array_equal(d.download(keep), data[off:off + keep])
+            off += r.symbols
+
+
+def test_fused_repeated_decodes(gpu, fused):
+    data = gpu.generate(13, 0.9, 3_000_000)
+    s = gpu.parse(gpu.encode(data))
+    with gpu.Decoder(0) as d:
+        d.load(s)
+        for _ in range(5):
+            d.decode()
+        r = d.report()
+        assert r.launches == 5 and r.status == 0 and r.symbols >= s.n
+        assert np.array_equal(d.download(s.n), data)
+
+
+def test_fused_corrupted_stream_terminates(gpu, fused):
+    data = gpu.generate(15, 0.9, 500_000)
+    img = gpu.encode(data).copy()
+    rng = np.random.default_rng(1)
+    hdr = 8 + 2 * len(gpu.parse(img).symbols) + 12
+    for pos in rng.integers(hdr, img.size, 200):
+        img[pos] ^= 0xFF
+    try:
+        out = gpu.decode(img)
+        assert out.size == data.size
+    except gpu.GapHuffError as e:
+        assert e.code in (-7, -2)
+
+
+@pytest.mark.parametrize("r", [0.9, 0.5])
+def test_fused_100MB(gpu, fused, r):
+    data = gpu.generate(375, r, 10**8)
+    assert np.array_equal(gpu.decode(gpu.encode(data)), data)
