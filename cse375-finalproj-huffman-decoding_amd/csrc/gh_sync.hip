@@ -18,22 +18,28 @@
 // on the device makes the raw stream decodable by the tuned count/write or tile
 // kernels unchanged; the count pass, scan and write pass are the hot path's own.
 //
-//  gh_sync_kernel      thread t starts decoding at the raw bit 128t (possibly
-//                      mid-codeword); walks of neighbouring threads then advance in
-//                      lock-step until they merge (below).  a_t = the entry offset
-//                      at 128(t+1) (the candidate gap[t]); b_t = the entry offset at
-//                      128(t+2) on the same walk.  Writes gap words and
-//                      pairs[t] = a_t | b_t << 4.
-//  gh_sync_fix_kernel  verification: b_t == a_{t+1} for every t proves every a_t
-//                      (induction: thread 0 starts at the true bit 0; if a_t is on
-//                      the true path then thread t's walk is true from there, so b_t
-//                      is the true entry at 128(t+2), which a_{t+1} equals).  A
-//                      mismatch is repaired by re-walking from b_t, following the
-//                      chain while it disagrees with the stored entries (the role of
-//                      CUHD's phase 2).  The host repeats the pass until it finds no
-//                      mismatch (CUHD's host loop, :439-475); on ordinary data the
-//                      first pass finds none.
-//  gh_sync_pack_kernel after repairs: pairs -> gap words.
+//  gh_sync_kernel      lane L owns the SYNC_M consecutive segments [L*M, L*M + M): one
+//                      continuous walk from the raw bit 128 (L*M - h) (h warm-up
+//                      segments, possibly mid-codeword; bit 0 for lane 0), recording the
+//                      entry at every boundary it passes inside its block as gap
+//                      nibbles (two gap words per lane), and its own view of the entry
+//                      at its block's first boundary L*M as check[L].  Codes
+//                      resynchronise within a few codewords, so after h segments the
+//                      walk is on the true path on ordinary data.  One walk per lane
+//                      from start to end: no lock-step rounds, no lanes idling while
+//                      neighbours' walks merge.
+//  gh_sync_fix_kernel  verification: check[L] == entry of boundary L*M as lane L-1
+//                      recorded it (its last nibble) for every L proves every nibble
+//                      (induction: lane 0 starts at the true bit 0; if lane L-1's
+//                      entries are true and lane L's walk stands on the same entry at
+//                      L*M, its walk is the true one from there).  A mismatch is
+//                      repaired by re-walking block L from the true entry until the
+//                      new entry equals the stored one (the walks merged: the rest is
+//                      true) or the block ends, then on into the next blocks while
+//                      they disagree (the role of CUHD's phase 2).  The host repeats
+//                      the pass until it finds no mismatch (CUHD's host loop,
+//                      :439-475); each pass makes at least the lowest mismatching block
+//                      true; on ordinary data the first pass finds none.
 //
 // One 13-bit LUT in LDS serves both walks: {step (the advance below, or the first
 // length when no codeword fits), length of the first codeword (0 if > 13 bits), bits of
@@ -55,8 +61,12 @@ namespace {
 
 constexpr int SK = 13;          // LUT prefix bits (12: cfg4 2.28 ms, 13: 2.08, 14: 3.10 - occupancy)
 constexpr int SYNC_TB = 256;    // threads per workgroup
-constexpr uint32_t SYNC_CHAIN = 256;  // segments one repair chain may walk per pass
-constexpr int SYNC_HALO = 8;          // warm-up segments per wave (GH_SYNC_HALO overrides)
+#ifndef GH_SYNC_M
+#define GH_SYNC_M 16
+#endif
+constexpr uint32_t SYNC_M = GH_SYNC_M;  // segments per lane (a multiple of 8: whole gap words)
+static_assert(SYNC_M % 8 == 0, "a lane writes whole gap words");
+constexpr int SYNC_HALO = 6;          // warm-up segments per lane (GH_SYNC_HALO overrides)
 
 #define GH_HIPS(expr)                                                             \
   do {                                                                            \
@@ -72,9 +82,9 @@ struct SyncParams {
   const uint16_t* lut;    // 1 << SK entries {step, first len << 5, multi-codeword advance << 10}
   uint32_t t13, t14, t15, t16;  // canonical left-aligned limits of lengths 13..16
   uint32_t* gaps;         // ceil(g / 8) gap words
-  uint32_t* pairs;        // g bytes {a | b << 4}, as words
+  uint8_t* check;         // ceil(g / SYNC_M): lane L's entry at boundary L * SYNC_M
   unsigned int* counter;  // mismatches found by a fix pass
-  uint32_t halo;          // warm-up segments per wave (multiple of 8, < 64)
+  uint32_t halo;          // warm-up segments per lane
 };
 
 __device__ __forceinline__ uint64_t ceil_div_d(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
@@ -158,148 +168,133 @@ __device__ __forceinline__ uint32_t walk_segment(uint64_t j, uint32_t off, const
   return walk_words<LONG>(w, off, lut, p);
 }
 
-// Each wavefront owns `out` = 64 - halo consecutive output segments [wo, wo+out); its
-// lanes walk segments [wo-halo, wo+out), so the first `halo` lanes are warm-up walks
-// that overlap the previous wave's segments.  Lane i's walk starts at the raw bit 128t
-// (t = wo-halo+i, possibly mid-codeword) and records its entry at boundary t+1.  Then,
-// in lock-step rounds (CUHD phase 1's scheme, cuhd_gpu_decoder.cu:186-229, here per
-// wavefront so no workgroup barrier is needed: a wave's LDS operations complete in
-// issue order), every walk that has not merged goes one segment on and compares its
-// entry with the record its right neighbour's walk left there: equal means the two
-// walks coincide from here on, so it stops; otherwise it overwrites the record (the
-// lower walk started earlier, so it is the one to keep).  Walks stop at boundary
-// wo+out+1 (the last b the wave needs).  The halo makes the wave's first output entry
-// come from a walk that started `halo` segments (128*halo bits) earlier, which on
-// ordinary codes has long merged with the true path, so the verify pass rarely finds a
-// seam to repair.
-constexpr int SYNC_WAVE = 64;
+// Words 4j..4j+4 of segment j, by value (kept in registers): seg_raw loads them with
+// the index clamped into the stream (no branch: the compiler then keeps the prefetch
+// in its own registers and waits for it only where it is used), seg_mask zeroes the
+// words past the stream once they have arrived.
+struct SegWords {
+  uint32_t w0, w1, w2, w3, w4;
+};
+__device__ __forceinline__ SegWords seg_raw(uint64_t j, const SyncParams& p) {
+  const uint64_t b = 4 * j, last = p.w - 1;  // (w >= 1 whenever a segment exists)
+  return {p.words[min(b, last)], p.words[min(b + 1, last)], p.words[min(b + 2, last)],
+          p.words[min(b + 3, last)], p.words[min(b + 4, last)]};
+}
+__device__ __forceinline__ SegWords seg_mask(const SegWords& r, uint64_t j, const SyncParams& p) {
+  const uint64_t b = 4 * j;
+  return {b < p.w ? r.w0 : 0u, b + 1 < p.w ? r.w1 : 0u, b + 2 < p.w ? r.w2 : 0u, b + 3 < p.w ? r.w3 : 0u,
+          b + 4 < p.w ? r.w4 : 0u};
+}
+
+// One step of a walk at segment-relative bit pos (< 128) over the segment's words and
+// the next segment's first word (w4): the multi-codeword advance unless it could pass
+// the boundary at 128, whose entry (the first start at or after it) is recorded; else
+// the first codeword's length.
+template <bool LONG>
+__device__ __forceinline__ uint32_t sync_step(uint32_t pos, const SegWords& w, const uint16_t* lut,
+                                              const SyncParams& p) {
+  // two-level select (a 64-bit half, then a word of it): a flat 4-way select of the
+  // words was turned into an indexed load from a private (scratch) copy
+  const bool h2 = pos >= 64u, w2nd = (pos & 32u) != 0;
+  const uint32_t ch = h2 ? w.w2 : w.w0, cl = h2 ? w.w3 : w.w1, nx = h2 ? w.w4 : w.w2;
+  const uint32_t a = w2nd ? cl : ch, b = w2nd ? nx : cl;
+  const uint32_t p16 = (uint32_t)(((((uint64_t)a << 32) | b) << (pos & 31u)) >> 48);
+  const uint32_t e = lut[p16 >> (16 - SK)];
+  const uint32_t adv = e >> 10;
+  uint32_t len = (e >> 5) & 31u;
+  if (LONG && len == 0) len = long_len(p16, p);
+  return (adv != 0 && pos + adv <= 128u) ? adv : len;
+}
+
 template <bool LONG>
 __global__ __launch_bounds__(SYNC_TB) void gh_sync_kernel(SyncParams p) {
   __shared__ uint16_t lut[1 << SK];
-  __shared__ uint8_t rec_all[SYNC_TB / SYNC_WAVE][SYNC_WAVE + 4];
-  stage_lut(lut, p.lut);
-  const uint32_t lane = threadIdx.x % SYNC_WAVE;
-  const uint32_t halo = p.halo, out = SYNC_WAVE - halo;
-  volatile uint8_t* rec = rec_all[threadIdx.x / SYNC_WAVE];
-  const uint64_t nwaves = ceil_div_d(p.g, out);
-  const uint64_t wstride = (uint64_t)gridDim.x * (SYNC_TB / SYNC_WAVE);
-  for (uint64_t wv = (uint64_t)blockIdx.x * (SYNC_TB / SYNC_WAVE) + threadIdx.x / SYNC_WAVE; wv < nwaves;
-       wv += wstride) {
-    const int64_t w0 = (int64_t)(wv * out) - (int64_t)halo;  // segment of lane 0
-    const int64_t ts = w0 + (int64_t)lane;
-    const uint64_t t = (uint64_t)ts;
-    const uint64_t kcap = (uint64_t)(w0 + SYNC_WAVE);  // last segment walked: boundary w0+65
-    bool active = ts >= 0 && t < p.g;
-    uint32_t off = 0;
-    uint64_t k = t + 1;  // boundary of the walk's current entry
-    if (lane < 4) rec[SYNC_WAVE + lane] = 0xff;
-    rec[lane] = 0xff;
-    __builtin_amdgcn_wave_barrier();
-    if (active) {
-      off = walk_segment<LONG>(t, 0, lut, p);
-      rec[lane] = (uint8_t)off;
-    }
-    __builtin_amdgcn_wave_barrier();
-    while (__any(active)) {
-      if (active) {
-        if (k > kcap || k >= p.g) {
-          active = false;
-        } else {
-          const uint32_t e = walk_segment<LONG>(k, off, lut, p);
-          ++k;
-          const uint32_t idx = (uint32_t)((int64_t)k - w0 - 1);
-          if (rec[idx] == e) {
-            active = false;
-          } else {
-            rec[idx] = (uint8_t)e;
-            off = e;
-          }
+  stage_lut(lut, p.lut);  // (the only barrier: lanes past the stream may leave after it)
+  const uint64_t L = (uint64_t)blockIdx.x * SYNC_TB + threadIdx.x;
+  const uint64_t sb = L * SYNC_M;  // the lane's block [sb, se)
+  if (sb >= p.g) return;
+  const uint64_t se = sb + SYNC_M < p.g ? sb + SYNC_M : p.g;
+  uint64_t s = sb > p.halo ? sb - p.halo : 0;  // segment of the walk; bit 0 of it is the start
+  uint32_t pos = 0;                           // segment-relative bit of the next codeword start
+  SegWords w = seg_mask(seg_raw(s, p), s, p), nx = seg_raw(s + 1, p);  // this segment's words, the next one's
+  uint32_t g0 = 0, g1 = 0, chk = 0;
+  while (__any(s < se)) {
+    if (s < se) {
+      pos += sync_step<LONG>(pos, w, lut, p);
+      if (pos >= 128u) {  // boundary 128 (s + 1) passed: its entry
+        uint32_t e = pos - 128u;
+        // no codeword crosses the end of the stream: the entry at 128g is 0, as the
+        // encoder leaves the last gap (encoder.cu:414 memset, nothing crosses 128G)
+        if (s + 1 >= p.g) e = 0;
+        if (s >= sb) {
+          const uint32_t k = (uint32_t)(s - sb);
+          if (k < 8) g0 |= e << (4 * k);
+          else g1 |= e << (4 * (k - 8));
+        } else if (s + 1 == sb) {
+          chk = e;
         }
+        ++s;
+        pos = e;
+        w = seg_mask(nx, s, p);
+        nx = seg_raw(s + 1, p);
       }
-      __builtin_amdgcn_wave_barrier();
     }
-    const bool mine = lane >= halo && ts >= 0 && t < p.g;
-    uint32_t a = 0, b = 0;
-    if (mine) {
-      a = rec[lane];
-      b = rec[lane + 1];
-      // no codeword crosses the end of the stream: the entry at 128g is 0, as the
-      // encoder leaves the last gap (encoder.cu:414 memset, nothing crosses 128G)
-      if (t + 1 >= p.g) a = 0;
-      if (t + 2 >= p.g) b = 0;
-    }
-    // w0 is a multiple of 8, so lane groups of 8 (4) are gap (pair) words
-    uint32_t v = a << (4 * (lane & 7));
-    v |= __shfl_xor(v, 1);
-    v |= __shfl_xor(v, 2);
-    v |= __shfl_xor(v, 4);
-    if ((lane & 7) == 0 && mine) p.gaps[t >> 3] = v;
-    uint32_t q = (a | b << 4) << (8 * (lane & 3));
-    q |= __shfl_xor(q, 1);
-    q |= __shfl_xor(q, 2);
-    if ((lane & 3) == 0 && mine) p.pairs[t >> 2] = q;
-    __builtin_amdgcn_wave_barrier();  // rec is reused by the wave's next segments
   }
+  const uint64_t gw = sb / 8, ngw = ceil_div_d(p.g, 8);
+  static_assert(SYNC_M == 16, "two gap words per lane");
+  p.gaps[gw] = g0;
+  if (gw + 1 < ngw) p.gaps[gw + 1] = g1;
+  p.check[L] = (uint8_t)chk;
 }
 
-__device__ __forceinline__ uint32_t pair_at(const uint32_t* pairs, uint64_t i) {
-  return (__atomic_load_n(pairs + (i >> 2), __ATOMIC_RELAXED) >> (8 * (i & 3))) & 0xffu;
+__device__ __forceinline__ uint32_t nib_at(const uint32_t* gaps, uint64_t i) {
+  return (__atomic_load_n(gaps + (i >> 3), __ATOMIC_RELAXED) >> (4 * (i & 7))) & 15u;
 }
 
-__device__ __forceinline__ void pair_store(uint32_t* pairs, uint64_t i, uint32_t v) {
-  uint32_t* wp = pairs + (i >> 2);
-  const uint32_t sh = 8 * (uint32_t)(i & 3);
+__device__ __forceinline__ void nib_store(uint32_t* gaps, uint64_t i, uint32_t v) {
+  uint32_t* wp = gaps + (i >> 3);
+  const uint32_t sh = 4 * (uint32_t)(i & 7);
   uint32_t old = __atomic_load_n(wp, __ATOMIC_RELAXED);
   for (;;) {
-    const uint32_t nw = (old & ~(0xffu << sh)) | (v << sh);
+    const uint32_t nw = (old & ~(15u << sh)) | (v << sh);
     const uint32_t seen = atomicCAS(wp, old, nw);
     if (seen == old) break;
     old = seen;
   }
 }
 
-// a_j := a (the entry at 128(j+1)); re-walk segment j+1 from it to get b_j, and keep
-// going while the new entry disagrees with the stored one.  (a, b) of one segment are
-// replaced together by one CAS, so a pass never sees a torn pair.
+// Block L re-walked from the entry a at boundary sb = L * SYNC_M (lane L-1's): every
+// entry that disagrees with the stored nibble is replaced, until a stored entry equals
+// the new one (lane L's walk merged with this one there: the rest of the block follows)
+// or the block ends; then check[L] := a.  Only lane L and this repair write block L's
+// nibbles, so once a is true (block L-1 verified) the block is true, and a later change
+// of a (block L-1 repaired after this) makes the next pass flag block L again.
 template <bool LONG>
-__device__ void repair_chain(uint64_t j, uint32_t a, const uint16_t* lut, const SyncParams& p) {
-  for (uint32_t s = 0; s < SYNC_CHAIN; ++s) {
-    uint32_t b = walk_segment<LONG>(j + 1, a, lut, p);
-    if (j + 2 >= p.g) b = 0;
-    pair_store(p.pairs, j, a | b << 4);
-    if (j + 2 >= p.g) break;
-    if ((pair_at(p.pairs, j + 1) & 15u) == b) break;  // back on the stored path
-    ++j;
-    a = b;
+__device__ void repair_block(uint64_t L, uint32_t a, const uint16_t* lut, const SyncParams& p) {
+  const uint64_t sb = L * SYNC_M, se = sb + SYNC_M < p.g ? sb + SYNC_M : p.g;
+  uint32_t entry = a;
+  for (uint64_t j = sb; j < se; ++j) {
+    uint32_t e = walk_segment<LONG>(j, entry, lut, p);
+    if (j + 1 >= p.g) e = 0;
+    if (nib_at(p.gaps, j) == e) break;  // merged
+    nib_store(p.gaps, j, e);
+    entry = e;
   }
+  p.check[L] = (uint8_t)a;
 }
 
 template <bool LONG>
 __global__ __launch_bounds__(SYNC_TB) void gh_sync_fix_kernel(SyncParams p) {
   __shared__ uint16_t lut[1 << SK];
   stage_lut(lut, p.lut);
-  if (p.g < 3) return;
+  const uint64_t nb = ceil_div_d(p.g, SYNC_M);
   const uint64_t stride = (uint64_t)gridDim.x * SYNC_TB;
-  for (uint64_t t = (uint64_t)blockIdx.x * SYNC_TB + threadIdx.x; t + 2 < p.g; t += stride) {
-    const uint32_t pt = pair_at(p.pairs, t), pn = pair_at(p.pairs, t + 1);
-    if ((pt >> 4) != (pn & 15u)) {
+  for (uint64_t L = (uint64_t)blockIdx.x * SYNC_TB + threadIdx.x + 1; L < nb; L += stride) {
+    const uint32_t a = nib_at(p.gaps, L * SYNC_M - 1);  // lane L-1's entry at boundary L * M
+    if (p.check[L] != a) {
       atomicAdd(p.counter, 1u);
-      repair_chain<LONG>(t + 1, pt >> 4, lut, p);
+      repair_block<LONG>(L, a, lut, p);
     }
-  }
-}
-
-__global__ __launch_bounds__(SYNC_TB) void gh_sync_pack_kernel(SyncParams p) {
-  const uint64_t nw = (p.g + 7) / 8;
-  const uint64_t stride = (uint64_t)gridDim.x * SYNC_TB;
-  for (uint64_t i = (uint64_t)blockIdx.x * SYNC_TB + threadIdx.x; i < nw; i += stride) {
-    uint32_t v = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < 8; ++k) {
-      const uint64_t s = 8 * i + k;
-      if (s + 1 < p.g) v |= (pair_at(p.pairs, s) & 15u) << (4 * k);
-    }
-    p.gaps[i] = v;
   }
 }
 
@@ -376,9 +371,10 @@ extern "C" int gh_sync_gaps(int device, const gh_sym* syms, uint32_t nsyms, cons
   hipStream_t st = (hipStream_t)hip_stream;
   SyncTables tabs;
   build_sync_tables(canon, tabs);
-  DevBuf lut, pairs, counter;
+  DevBuf lut, check, counter;
+  const uint64_t nblk = ceil_div(g, (uint64_t)SYNC_M);  // lanes of the walk kernel
   GH_HIPS(hipMalloc(&lut.p, 2u << SK));
-  GH_HIPS(hipMalloc(&pairs.p, 4 * ceil_div(g, 4) + 16));
+  GH_HIPS(hipMalloc(&check.p, nblk + 16));
   GH_HIPS(hipMalloc(&counter.p, 16));
   GH_HIPS(hipMemcpyAsync(lut.p, tabs.lut.data(), 2u << SK, hipMemcpyHostToDevice, st));
   SyncParams p{};
@@ -391,12 +387,12 @@ extern "C" int gh_sync_gaps(int device, const gh_sym* syms, uint32_t nsyms, cons
   p.t15 = tabs.T[15];
   p.t16 = tabs.T[16];
   p.gaps = d_gap_words;
-  p.pairs = (uint32_t*)pairs.p;
+  p.check = (uint8_t*)check.p;
   p.counter = (unsigned int*)counter.p;
   {
     const char* eh = getenv("GH_SYNC_HALO");
     const int h = eh ? atoi(eh) : SYNC_HALO;
-    p.halo = (uint32_t)std::clamp(h - h % 8, 0, 56);
+    p.halo = (uint32_t)std::clamp(h, 0, 64);
   }
   hipEvent_t e0, e1;
   GH_HIPS(hipEventCreate(&e0));
@@ -408,8 +404,8 @@ extern "C" int gh_sync_gaps(int device, const gh_sym* syms, uint32_t nsyms, cons
   const bool lng = canon.maxlen > (uint32_t)SK;
   const void* ks = lng ? (const void*)gh_sync_kernel<true> : (const void*)gh_sync_kernel<false>;
   const void* kf = lng ? (const void*)gh_sync_fix_kernel<true> : (const void*)gh_sync_fix_kernel<false>;
-  const int gs = grid_for(ks, ceil_div(g, SYNC_WAVE - p.halo) * SYNC_WAVE);
-  const int gf = grid_for(kf, g);
+  const int gs = (int)ceil_div(nblk, (uint64_t)SYNC_TB);  // one lane per block (not persistent)
+  const int gf = grid_for(kf, nblk);
   void* kargs[] = {&p};
   GH_HIPS(hipMemsetAsync(counter.p, 0, 4, st));
   GH_HIPS(hipEventRecord(e0, st));
@@ -429,16 +425,10 @@ extern "C" int gh_sync_gaps(int device, const gh_sym* syms, uint32_t nsyms, cons
     ++passes;
     if (cnt == 0) break;
     mism += cnt;
-    // each pass makes at least one more boundary true (the first mismatch follows a
-    // true entry), so g passes always suffice
-    if (passes > g + 1) return fail(GH_E_CORRUPT, "self-synchronisation did not converge");
+    // each pass makes at least the lowest mismatching block true, so nblk passes
+    // always suffice
+    if (passes > nblk + 1) return fail(GH_E_CORRUPT, "self-synchronisation did not converge");
     GH_HIPS(hipMemsetAsync(counter.p, 0, 4, st));
-  }
-  if (mism) {
-    hipLaunchKernelGGL(gh_sync_pack_kernel, dim3(grid_for((const void*)gh_sync_pack_kernel, ceil_div(g, 8))),
-                       dim3(SYNC_TB), 0, st, p);
-    GH_HIPS(hipGetLastError());
-    GH_HIPS(hipStreamSynchronize(st));
   }
   if (rep) {
     rep->mismatches = mism;

@@ -33,3 +33,17 @@ for label, sel in [("all", np.ones(grid, bool)), ("WG < grid/2", np.arange(grid)
         tot = d.sum(axis=1).mean()
         parts = "  ".join(f"{n} {d[:, i].mean():7.0f}" for i, n in enumerate(names))
         print(f"{label:13s} wave {4 * wv}: total {tot:7.0f} | {parts}")
+# per-workgroup sums over its iterations (wave 0): a grid whose rounds wait for the
+# slowest workgroup shows it as the workgroups that never wait for a prefix
+w0 = a[:, 0, :, :] * valid[:, 0, :, None]
+busy = w0.sum(axis=(1, 2)) - w0[:, :, 3].sum(axis=1)
+pref = w0[:, :, 3].sum(axis=1)
+iters = valid[:, 0, :].sum(axis=1)
+sel = iters > 0
+q = [0, 1, 10, 50, 90, 99, 100]
+print("per-WG iterations   ", np.percentile(iters[sel], q).round(0))
+print("per-WG busy cycles  ", np.percentile(busy[sel], q).round(-3))
+print("per-WG prefix cycles", np.percentile(pref[sel], q).round(-3))
+slow = np.argsort(busy[sel])[-8:]
+print("slowest WGs (busy)  ", np.nonzero(sel)[0][slow], busy[sel][slow].round(-3))
+

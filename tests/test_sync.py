@@ -223,7 +223,7 @@ def test_gpu_decode_raw_large_property(gpu, orc):
 @pytest.mark.gpu
 @pytest.mark.parametrize("halo", ["0", "8", "56"])
 def test_gpu_sync_halo_variants(gpu, orc, halo, monkeypatch):
-    """Warm-up lanes per wave (GH_SYNC_HALO) change only how much the verify pass has to
+    """Warm-up segments per lane (GH_SYNC_HALO) change only how much the verify pass has to
     repair, never the gaps."""
     monkeypatch.setenv("GH_SYNC_HALO", halo)
     d = orc.generate(9, 0.5, 400_009)
