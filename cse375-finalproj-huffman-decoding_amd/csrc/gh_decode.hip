@@ -832,7 +832,7 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     static thread_local TileParams tp;
     tp = t;
     ta[0] = &tp;
-    GH_HIP(hipLaunchKernel(kern, dim3(c->grid), dim3(TILE_TB), ta, c->lds, st));
+    GH_HIP(hipLaunchKernel(kern, dim3(c->grid), dim3(c->ftile ? FT_TB : TILE_TB), ta, c->lds, st));
     GH_HIP(hipEventRecord(dc.last, st));
     dc.has = true;
   }

@@ -83,7 +83,7 @@ struct SyncParams {
   uint32_t t13, t14, t15, t16;  // canonical left-aligned limits of lengths 13..16
   uint32_t* gaps;         // ceil(g / 8) gap words
   uint8_t* check;         // ceil(g / SYNC_M): lane L's entry at boundary L * SYNC_M
-  unsigned int* counter;  // mismatches found by a fix pass
+  unsigned int* counter;  // [0] fix-pass mismatches, [1] repairs reaching a wave's end, [2] in-wave mismatches
   uint32_t halo;          // warm-up segments per lane
 };
 
@@ -186,65 +186,138 @@ __device__ __forceinline__ SegWords seg_mask(const SegWords& r, uint64_t j, cons
           b + 4 < p.w ? r.w4 : 0u};
 }
 
-// One step of a walk at segment-relative bit pos (< 128) over the segment's words and
-// the next segment's first word (w4): the multi-codeword advance unless it could pass
-// the boundary at 128, whose entry (the first start at or after it) is recorded; else
-// the first codeword's length.
-template <bool LONG>
-__device__ __forceinline__ uint32_t sync_step(uint32_t pos, const SegWords& w, const uint16_t* lut,
-                                              const SyncParams& p) {
-  // two-level select (a 64-bit half, then a word of it): a flat 4-way select of the
-  // words was turned into an indexed load from a private (scratch) copy
-  const bool h2 = pos >= 64u, w2nd = (pos & 32u) != 0;
-  const uint32_t ch = h2 ? w.w2 : w.w0, cl = h2 ? w.w3 : w.w1, nx = h2 ? w.w4 : w.w2;
-  const uint32_t a = w2nd ? cl : ch, b = w2nd ? nx : cl;
-  const uint32_t p16 = (uint32_t)(((((uint64_t)a << 32) | b) << (pos & 31u)) >> 48);
-  const uint32_t e = lut[p16 >> (16 - SK)];
-  const uint32_t adv = e >> 10;
-  uint32_t len = (e >> 5) & 31u;
-  if (LONG && len == 0) len = long_len(p16, p);
-  return (adv != 0 && pos + adv <= 128u) ? adv : len;
+// One word of the wave's walks in step: q (< 32, else the lane is past this word) is
+// the next codeword start relative to the top of hi; loops until every lane is past
+// the word and returns q - 32, the start relative to the next word.  hi:lo is fixed
+// for the word, so a step is a 64-bit shift, one LDS read and an add.  BOUND (the
+// segment's last word): the start at or after the boundary is recorded, so no
+// multi-codeword step may pass it.
+template <bool BOUND, bool LONG>
+__device__ __forceinline__ uint32_t walk_word_ls(uint32_t hi, uint32_t lo, uint32_t q, const uint16_t* lut,
+                                                 const SyncParams& p) {
+  const uint64_t win = ((uint64_t)hi << 32) | lo;
+  while (__any(q < 32u)) {  // branch-free body: lanes past the word look up harmlessly
+    const uint32_t p16 = (uint32_t)((win << (q & 31u)) >> 48);
+    const uint32_t e = lut[p16 >> (16 - SK)];
+    uint32_t st;
+    if constexpr (!BOUND) {
+      st = e & 31u;  // precomputed: the advance if any, else the first length
+      if (LONG && st == 0) st = long_len(p16, p);
+    } else {
+      const uint32_t adv = e >> 10;
+      uint32_t len = (e >> 5) & 31u;
+      if (LONG && len == 0) len = long_len(p16, p);
+      st = (adv != 0 && q + adv <= 32u) ? adv : len;
+    }
+    q += q < 32u ? st : 0u;
+  }
+  return q - 32u;
 }
 
+// The lanes of a wave walk their blocks in step: iteration i walks segment
+// sb - h + i of every lane (a lane whose walk would start before segment 0 idles until
+// it reaches segment 0, then starts at the true bit 0), so the next segments' loads are
+// issued by the whole wave at once, two segments ahead, and waited for with a counted
+// vmcnt.  (Lanes crossing boundaries at different steps, each loading its next
+// segment then, made every step wait for the latest lane's loads: 1.7 ms on cfg4.)
 template <bool LONG>
 __global__ __launch_bounds__(SYNC_TB) void gh_sync_kernel(SyncParams p) {
   __shared__ uint16_t lut[1 << SK];
-  stage_lut(lut, p.lut);  // (the only barrier: lanes past the stream may leave after it)
+  stage_lut(lut, p.lut);  // (the only barrier: waves past the stream may leave after it)
   const uint64_t L = (uint64_t)blockIdx.x * SYNC_TB + threadIdx.x;
   const uint64_t sb = L * SYNC_M;  // the lane's block [sb, se)
-  if (sb >= p.g) return;
-  const uint64_t se = sb + SYNC_M < p.g ? sb + SYNC_M : p.g;
-  uint64_t s = sb > p.halo ? sb - p.halo : 0;  // segment of the walk; bit 0 of it is the start
-  uint32_t pos = 0;                           // segment-relative bit of the next codeword start
-  SegWords w = seg_mask(seg_raw(s, p), s, p), nx = seg_raw(s + 1, p);  // this segment's words, the next one's
-  uint32_t g0 = 0, g1 = 0, chk = 0;
-  while (__any(s < se)) {
-    if (s < se) {
-      pos += sync_step<LONG>(pos, w, lut, p);
-      if (pos >= 128u) {  // boundary 128 (s + 1) passed: its entry
-        uint32_t e = pos - 128u;
-        // no codeword crosses the end of the stream: the entry at 128g is 0, as the
-        // encoder leaves the last gap (encoder.cu:414 memset, nothing crosses 128G)
-        if (s + 1 >= p.g) e = 0;
-        if (s >= sb) {
-          const uint32_t k = (uint32_t)(s - sb);
-          if (k < 8) g0 |= e << (4 * k);
-          else g1 |= e << (4 * (k - 8));
-        } else if (s + 1 == sb) {
-          chk = e;
+  if (__builtin_amdgcn_readfirstlane((uint32_t)(sb - (uint64_t)(threadIdx.x % 64) * SYNC_M >= p.g))) return;
+  const uint64_t se = sb < p.g ? (sb + SYNC_M < p.g ? sb + SYNC_M : p.g) : sb;  // (empty past the stream)
+  const int64_t s0 = (int64_t)sb - (int64_t)p.halo;  // segment of iteration 0
+  auto seg_at = [&](int64_t s) { return (uint64_t)(s < 0 ? 0 : s); };
+  SegWords w = seg_raw(seg_at(s0), p), n1 = seg_raw(seg_at(s0 + 1), p);
+  w = seg_mask(w, seg_at(s0), p);
+  uint32_t pos = 0;  // segment-relative bit of the next codeword start
+  uint32_t g0 = 0, g1 = 0, g2 = 0, g3 = 0, chk = 0;
+  const int nit = (int)p.halo + (int)SYNC_M;
+  for (int i = 0; i < nit; ++i) {
+    const int64_t s = s0 + i;
+    const SegWords n2 = seg_raw(seg_at(s + 2), p);  // two segments ahead
+    const bool act = s >= 0 && s < (int64_t)se;
+    // an idle lane walks nothing: q starts past every word (and stays there)
+    uint32_t q = act ? pos : 512u;
+    q = walk_word_ls<false, LONG>(w.w0, w.w1, q, lut, p);
+    q = walk_word_ls<false, LONG>(w.w1, w.w2, q, lut, p);
+    q = walk_word_ls<false, LONG>(w.w2, w.w3, q, lut, p);
+    q = walk_word_ls<true, LONG>(w.w3, w.w4, q, lut, p);
+    if (act) {  // boundary 128 (s + 1) passed: its entry
+      uint32_t e = q;
+      // no codeword crosses the end of the stream: the entry at 128g is 0, as the
+      // encoder leaves the last gap (encoder.cu:414 memset, nothing crosses 128G)
+      if ((uint64_t)s + 1 >= p.g) e = 0;
+      if ((uint64_t)s >= sb) {
+        const uint32_t k = (uint32_t)((uint64_t)s - sb);
+        if (k < 8) g0 |= e << (4 * k);
+        else if (k < 16) g1 |= e << (4 * (k - 8));
+        else if (k < 24) g2 |= e << (4 * (k - 16));
+        else g3 |= e << (4 * (k - 24));
+      } else if ((uint64_t)s + 1 == sb) {
+        chk = e;
+      }
+      pos = e;
+    }
+    w = seg_mask(n1, seg_at(s + 1), p);
+    n1 = n2;
+  }
+  // Verify and repair inside the wave: lane l's view of the entry at its block's start
+  // (chk) against lane l-1's last nibble.  A mismatching block is re-walked from that
+  // entry, in step with the wave's other mismatching blocks, until a recorded entry
+  // equals the new one (the walks merged) or the block ends; rounds repeat while a
+  // block's left neighbour changed.  Lane 0's block is verified by gh_sync_fix_kernel
+  // against the previous wave's last block.
+  auto nib_get = [&](int k) {
+    const uint32_t gw_ = k < 8 ? g0 : k < 16 ? g1 : k < 24 ? g2 : g3;
+    return (gw_ >> (4 * (k & 7))) & 15u;
+  };
+  auto nib_set = [&](int k, uint32_t v) {
+    uint32_t& gw_ = k < 8 ? g0 : k < 16 ? g1 : k < 24 ? g2 : g3;
+    gw_ = (gw_ & ~(15u << (4 * (k & 7)))) | (v << (4 * (k & 7)));
+  };
+  const uint32_t lane = threadIdx.x % 64;
+  for (int round = 0; round < 64; ++round) {
+    const uint32_t left = (uint32_t)__shfl_up((int)nib_get(SYNC_M - 1), 1);
+    const bool bad = lane > 0 && sb < p.g && chk != left;
+    if (!__any(bad)) break;
+    if (bad) atomicAdd(p.counter + 2, 1u);  // (reported as mismatches)
+    bool run = bad;
+    uint32_t e = left;
+#pragma unroll
+    for (int k = 0; k < (int)SYNC_M; ++k) {
+      if (!__any(run)) break;
+      const uint64_t s = sb + (uint64_t)k;
+      run = run && s < se;
+      const SegWords ws = seg_mask(seg_raw(run ? s : 0, p), run ? s : 0, p);
+      uint32_t q = run ? e : 512u;
+      q = walk_word_ls<false, LONG>(ws.w0, ws.w1, q, lut, p);
+      q = walk_word_ls<false, LONG>(ws.w1, ws.w2, q, lut, p);
+      q = walk_word_ls<false, LONG>(ws.w2, ws.w3, q, lut, p);
+      q = walk_word_ls<true, LONG>(ws.w3, ws.w4, q, lut, p);
+      if (run) {
+        const uint32_t e2 = s + 1 >= p.g ? 0u : q;
+        if (nib_get(k) == e2) {
+          run = false;  // merged: the rest of the block follows
+        } else {
+          nib_set(k, e2);
+          e = e2;
         }
-        ++s;
-        pos = e;
-        w = seg_mask(nx, s, p);
-        nx = seg_raw(s + 1, p);
       }
     }
+    if (bad) chk = left;
   }
-  const uint64_t gw = sb / 8, ngw = ceil_div_d(p.g, 8);
-  static_assert(SYNC_M == 16, "two gap words per lane");
-  p.gaps[gw] = g0;
-  if (gw + 1 < ngw) p.gaps[gw + 1] = g1;
-  p.check[L] = (uint8_t)chk;
+  if (sb < p.g) {
+    const uint64_t gw = sb / 8, ngw = ceil_div_d(p.g, 8);
+    static_assert(SYNC_M == 16 || SYNC_M == 24 || SYNC_M == 32, "two to four gap words per lane");
+    p.gaps[gw] = g0;
+    if (gw + 1 < ngw) p.gaps[gw + 1] = g1;
+    if (SYNC_M > 16 && gw + 2 < ngw) p.gaps[gw + 2] = g2;
+    if (SYNC_M > 24 && gw + 3 < ngw) p.gaps[gw + 3] = g3;
+    p.check[L] = (uint8_t)chk;
+  }
 }
 
 __device__ __forceinline__ uint32_t nib_at(const uint32_t* gaps, uint64_t i) {
@@ -283,17 +356,26 @@ __device__ void repair_block(uint64_t L, uint32_t a, const uint16_t* lut, const 
   p.check[L] = (uint8_t)a;
 }
 
+// The walk kernel verified every block against its left neighbour inside its wave; a
+// thread here takes one wave's first block (its left neighbour is the previous wave's
+// last) and, while a repaired block's successor no longer agrees, the wave's next
+// blocks.  counter[0]: mismatching blocks; counter[1]: repairs that reached a wave's
+// last block (whose successor, another wave's first block, must then be verified
+// again: the host repeats the pass while it is non-zero).
 template <bool LONG>
 __global__ __launch_bounds__(SYNC_TB) void gh_sync_fix_kernel(SyncParams p) {
   __shared__ uint16_t lut[1 << SK];
   stage_lut(lut, p.lut);
-  const uint64_t nb = ceil_div_d(p.g, SYNC_M);
+  const uint64_t nb = ceil_div_d(p.g, SYNC_M), nwv = ceil_div_d(nb, 64);
   const uint64_t stride = (uint64_t)gridDim.x * SYNC_TB;
-  for (uint64_t L = (uint64_t)blockIdx.x * SYNC_TB + threadIdx.x + 1; L < nb; L += stride) {
-    const uint32_t a = nib_at(p.gaps, L * SYNC_M - 1);  // lane L-1's entry at boundary L * M
-    if (p.check[L] != a) {
+  for (uint64_t k = (uint64_t)blockIdx.x * SYNC_TB + threadIdx.x + 1; k < nwv; k += stride) {
+    const uint64_t L1 = min(64 * k + 64, nb);
+    for (uint64_t L = 64 * k; L < L1; ++L) {
+      const uint32_t a = nib_at(p.gaps, L * SYNC_M - 1);  // block L-1's entry at boundary L * M
+      if (p.check[L] == a) break;
       atomicAdd(p.counter, 1u);
       repair_block<LONG>(L, a, lut, p);
+      if (L + 1 == L1) atomicAdd(p.counter + 1, 1u);
     }
   }
 }
@@ -405,9 +487,9 @@ extern "C" int gh_sync_gaps(int device, const gh_sym* syms, uint32_t nsyms, cons
   const void* ks = lng ? (const void*)gh_sync_kernel<true> : (const void*)gh_sync_kernel<false>;
   const void* kf = lng ? (const void*)gh_sync_fix_kernel<true> : (const void*)gh_sync_fix_kernel<false>;
   const int gs = (int)ceil_div(nblk, (uint64_t)SYNC_TB);  // one lane per block (not persistent)
-  const int gf = grid_for(kf, nblk);
+  const int gf = grid_for(kf, ceil_div(nblk, (uint64_t)64));  // one thread per wave of the walk
   void* kargs[] = {&p};
-  GH_HIPS(hipMemsetAsync(counter.p, 0, 4, st));
+  GH_HIPS(hipMemsetAsync(counter.p, 0, 12, st));
   GH_HIPS(hipEventRecord(e0, st));
   GH_HIPS(hipLaunchKernel(ks, dim3(gs), dim3(SYNC_TB), kargs, 0, st));
   GH_HIPS(hipGetLastError());
@@ -418,17 +500,17 @@ extern "C" int gh_sync_gaps(int device, const gh_sym* syms, uint32_t nsyms, cons
     GH_HIPS(hipLaunchKernel(kf, dim3(gf), dim3(SYNC_TB), kargs, 0, st));
     GH_HIPS(hipGetLastError());
     GH_HIPS(hipEventRecord(e1, st));
-    unsigned int cnt = 0;
-    GH_HIPS(hipMemcpyAsync(&cnt, counter.p, 4, hipMemcpyDeviceToHost, st));
+    unsigned int cnt[3] = {};
+    GH_HIPS(hipMemcpyAsync(cnt, counter.p, 12, hipMemcpyDeviceToHost, st));
     GH_HIPS(hipStreamSynchronize(st));
     GH_HIPS(hipEventElapsedTime(&ms, e0, e1));
     ++passes;
-    if (cnt == 0) break;
-    mism += cnt;
-    // each pass makes at least the lowest mismatching block true, so nblk passes
-    // always suffice
-    if (passes > nblk + 1) return fail(GH_E_CORRUPT, "self-synchronisation did not converge");
-    GH_HIPS(hipMemsetAsync(counter.p, 0, 4, st));
+    mism += cnt[0] + (passes == 1 ? cnt[2] : 0u);
+    if (cnt[1] == 0) break;  // no repair reached a wave's last block: every block verified
+    // each pass makes at least the lowest mismatching wave true, so one pass per wave
+    // always suffices
+    if (passes > nblk / 64 + 2) return fail(GH_E_CORRUPT, "self-synchronisation did not converge");
+    GH_HIPS(hipMemsetAsync(counter.p, 0, 8, st));
   }
   if (rep) {
     rep->mismatches = mism;

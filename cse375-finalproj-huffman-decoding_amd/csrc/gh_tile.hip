@@ -35,7 +35,10 @@
 
 // Build knobs (make variant VFLAGS=-D...; every alternative value is measured in
 // DESIGN.md's tile-kernel section, the defaults are the fastest).
-constexpr int TILE_TB = 512;       // threads per workgroup
+#ifndef GH_TILE_TB
+#define GH_TILE_TB 512
+#endif
+constexpr int TILE_TB = GH_TILE_TB;  // threads per workgroup
 #ifndef GH_TILE_U
 #define GH_TILE_U 3
 #endif
@@ -63,6 +66,9 @@ constexpr int TILE_SCAP = GH_TILE_SCAPB;  // staging bytes per segment (larger t
 #endif
 #ifndef GH_TILE_PHI
 #define GH_TILE_PHI 2
+#endif
+#ifndef GH_TILE_ALTPRIO
+#define GH_TILE_ALTPRIO 0
 #endif
 #ifndef GH_TILE_PLO
 #define GH_TILE_PLO 0
@@ -663,7 +669,14 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE,
       break;
     }
     const uint32_t par = k & 1u;
-    if (GH_TILE_WPRIO && wid >= 4) {
+    if (GH_TILE_ALTPRIO) {
+      // the two workgroups of a CU (whichever they are: consecutive indices or 256
+      // apart) take turns at the higher issue priority, so the younger one is not
+      // always second (it otherwise ran ~5 % slower and the rounds waited for it)
+      const uint32_t turn = (k + blockIdx.x + (blockIdx.x >> 8)) & 1u;
+      if (turn) __builtin_amdgcn_s_setprio(2);
+      else __builtin_amdgcn_s_setprio(1);
+    } else if (GH_TILE_WPRIO && wid >= 4) {
       if (ahead) __builtin_amdgcn_s_setprio(GH_TILE_PLO + 1);
       else __builtin_amdgcn_s_setprio(GH_TILE_PHI + 1);
     } else {

@@ -32,10 +32,27 @@ def fused(monkeypatch):
     monkeypatch.setenv("GH_MODE", "fused")
 
 
+def _complete(syms):
+    return sum(2.0 ** -l for _, l in syms) == 1.0
+
+
+def _takes(syms):  # the fused kernel's codes: complete, codewords within its tables (12 bits)
+    return _complete(syms) and max(l for _, l in syms) <= 12
+
+
 @pytest.mark.parametrize("r", [0.5, 0.9, 0.999])
 @pytest.mark.parametrize("n", [1, 2, 7, 100, 4097, 65549, 1_000_003, 5_000_011])
 def test_fused_vs_oracle(gpu, orc, fused, r, n):
-    img = _check(gpu, orc, gpu.generate(2000 + n, r, n))
+    """Complete codes decode bit-exact; an incomplete one (e.g. the one-symbol code of a
+    tiny input) or one with codewords longer than the tables is refused at load (the
+    wave split's canonical fallback takes those)."""
+    data = gpu.generate(2000 + n, r, n)
+    img = gpu.encode(data)
+    if not _takes(gpu.parse(img).symbols):
+        with pytest.raises(gpu.GapHuffError):
+            gpu.decode(img)
+        return
+    _check(gpu, orc, data)
     rep = _report(gpu, img)
     assert gpu.MODE_NAMES[rep.mode] == "fused" and rep.status == 0
 
@@ -44,7 +61,9 @@ def test_fused_small_codes(gpu, orc, fused):
     # one-bit codes (two symbols: 128 codewords per segment), 8-bit codes, and a
     # segment-multiple stream
     rng = np.random.default_rng(3)
-    _check(gpu, orc, (rng.integers(0, 2, 300_001) + 48).astype(np.uint8))
+    two = (rng.integers(0, 2, 300_001) + 48).astype(np.uint8)
+    assert _complete(gpu.parse(gpu.encode(two)).symbols)
+    _check(gpu, orc, two)
     data = np.tile(np.arange(256, dtype=np.uint8), 64)
     rng.shuffle(data)
     _check(gpu, orc, data)
