@@ -300,8 +300,8 @@ static uint32_t ws_count_bits(const Canon& cn) {
 // lookups per window shift over ~13 ops per lookup plus ~12 per shift; a wider table
 // must win by 5 % (its LDS costs occupancy).  GH_WS_K overrides (tests).
 static uint32_t ws_write_bits(const Canon& cn) {
-  if (const char* ek = getenv("GH_WS_K"))
-    return (uint32_t)std::clamp(atoi(ek), (int)std::min<uint32_t>(std::max<uint32_t>(cn.maxlen, 2), 12), 12);
+  if (const char* ek = getenv("GH_WS_K"))  // (a width below maxlen takes the canonical fallback)
+    return (uint32_t)std::clamp(atoi(ek), 2, 12);
   const uint32_t lo = std::min<uint32_t>(std::max<uint32_t>(cn.maxlen, 10), 12);
   uint32_t best = lo;
   double best_eff = -1;

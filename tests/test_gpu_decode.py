@@ -222,11 +222,12 @@ def test_graft_smoke(gpu):
     __graft_entry__.smoke()
 
 
-@pytest.mark.parametrize("k", ["", "10", "11", "12"])
+@pytest.mark.parametrize("k", ["", "8", "10", "11", "12"])
 @pytest.mark.parametrize("stage", ["", "1"])
 @pytest.mark.parametrize("grid", ["", "1", "3"])
 def test_wave_split_widths_and_staging(gpu, orc, k, stage, grid, monkeypatch):
-    """The wave split at every write-LUT width (GH_WS_K), with the default staging and
+    """The wave split at every write-LUT width (GH_WS_K; below maxlen the canonical
+    fallback takes the longer codewords), with the default staging and
     with the staging forced down to one chain's worst case, so that blocks are staged
     one chain at a time (GH_WS_STAGE), on the default grid and on grids of 1 and 3
     workgroups (GH_WS_GRID: each wave walks many blocks)."""
