@@ -142,9 +142,6 @@ struct gh_ctx {
   uint32_t* d_lut_t = nullptr;
   uint4* d_tile_junk = nullptr;    // one 16-byte slot per thread of the grid
   uint4* d_stamps = nullptr;       // GH_TILE_STAMPS builds only
-  unsigned int* d_tile_cnt = nullptr;  // GH_TILE_DYN builds: per-round ticket counters, two parities
-  uint32_t* d_tile_scratch = nullptr;  // GH_TILE_DYN builds: tiles larger than the staging
-  uint32_t tile_nrounds = 0;
   // fused tile kernel (c->tile and c->ftile): the wave split's tables, one staging
   bool ftile = false;
   uint32_t ft_kc = 0, ft_kw = 0, ft_lutw_off = 0, ft_lutw_bytes = 0, ft_stage_off = 0;
@@ -176,7 +173,7 @@ struct gh_ctx {
 static void free_shard(gh_ctx* c) {
   (void)hipSetDevice(c->device);
   for (void* p : {(void*)c->d_payload, (void*)c->d_gaps, (void*)c->d_out, (void*)c->d_gran, (void*)c->d_lut_t,
-                  (void*)c->d_tile_junk, (void*)c->d_stamps, (void*)c->d_tile_cnt, (void*)c->d_tile_scratch, (void*)c->d_ws_lut_c, (void*)c->d_ws_lut_w, (void*)c->d_fb,
+                  (void*)c->d_tile_junk, (void*)c->d_stamps, (void*)c->d_ws_lut_c, (void*)c->d_ws_lut_w, (void*)c->d_fb,
                   (void*)c->d_seg_cnt, (void*)c->d_ws_junk, (void*)c->d_rng_tot, (void*)c->d_rng_off})
     (void)hipFree(p);
   c->d_payload = nullptr;
@@ -186,8 +183,6 @@ static void free_shard(gh_ctx* c) {
   c->d_lut_t = nullptr;
   c->d_tile_junk = nullptr;
   c->d_stamps = nullptr;
-  c->d_tile_cnt = nullptr;
-  c->d_tile_scratch = nullptr;
   c->d_ws_lut_c = nullptr;
   c->d_ws_lut_w = nullptr;
   c->d_fb = nullptr;
@@ -262,13 +257,6 @@ static int tile_setup(gh_ctx* c, uint32_t K, double avg_seg_bytes) {
   if (GH_TILE_STAMPS) {
     GH_HIP(hipMalloc(&c->d_stamps, 32ull * c->grid * 2 * 128));
     GH_HIP(hipMemset(c->d_stamps, 0, 32ull * c->grid * 2 * 128));
-  }
-  c->tile_nrounds = (uint32_t)ceil_div((uint64_t)c->ntiles, (uint64_t)c->grid - 1);
-  if (GH_TILE_DYN) {
-    const uint64_t ow = c->tile_minl >= 4 ? 8 : 11;
-    GH_HIP(hipMalloc(&c->d_tile_cnt, 8ull * (c->tile_nrounds + 4)));
-    GH_HIP(hipMemset(c->d_tile_cnt, 0, 8ull * (c->tile_nrounds + 4)));
-    GH_HIP(hipMalloc(&c->d_tile_scratch, 4ull * c->grid * 2 * TILE_TB * c->tile_u * (ow + 2)));
   }
   c->tile = true;
   return GH_OK;
@@ -386,9 +374,37 @@ static int ws_ns_for(double avg_seg_bytes) {
   return ns <= 2 ? 2 : ns <= 3 ? 3 : ns <= 4 ? 4 : ns <= 6 ? 6 : 8;
 }
 
+// Codes that take the canonical fallback anyway (longer than 12 bits, or incomplete):
+// the write LUT may be narrower than maxlen.  GH_WS_FBOCC=1 picks the widest width >= 8
+// whose LUT leaves room for one more write workgroup per CU (one chain's worst-case
+// staging per wave): long-code streams of one-bit codewords otherwise run one workgroup
+// per CU behind a 32 KB table.
+static uint32_t ws_fb_write_bits(const Canon& cn, uint32_t K, double avg_seg_bytes) {
+  const char* e = getenv("GH_WS_FBOCC");
+  if (!e || atoi(e) == 0 || getenv("GH_WS_K")) return K;
+  const uint32_t maxsyms = std::min<uint32_t>(143 / std::max<uint32_t>(cn.minlen, 1) + 1, 255);
+  const size_t chain_worst = 64ull * maxsyms + 64;
+  const size_t typical = (size_t)(1.3 * avg_seg_bytes * 64 * WS_U) + 64;
+  const size_t want = std::max(chain_worst, std::min<size_t>(64ull * WS_U * maxsyms + 64, typical));
+  constexpr int NW = WS_TB / 64;
+  auto wgs = [&](uint32_t k, size_t need) {
+    const long lb = (long)(8ull << k) + (long)FB_BYTES;
+    int best = 0;
+    for (int wg = 8; wg >= 1 && !best; --wg)
+      if (((long)(163840 / wg) - lb) / NW >= (long)need) best = wg;
+    return best;
+  };
+  const int base = std::max(wgs(K, want), wgs(K, chain_worst));
+  for (uint32_t k = K; k >= 8; --k)
+    if (wgs(k, chain_worst) > base) return k;
+  return K;
+}
+
 static int ws_setup(gh_ctx* c, double avg_seg_bytes) {
   const Canon& cn = c->canon;
-  const uint32_t K = ws_write_bits(cn), kc = ws_count_bits(cn);
+  const uint32_t kc = ws_count_bits(cn);
+  uint32_t K = ws_write_bits(cn);
+  if (kraft16(cn) != 65536 || cn.maxlen > std::min(K, kc)) K = ws_fb_write_bits(cn, K, avg_seg_bytes);
   // canonical fallback: codewords longer than a table, or patterns outside an incomplete
   // code (a LUT entry with no codeword)
   const bool fb = kraft16(cn) != 65536 || cn.maxlen > std::min(K, kc);
@@ -747,7 +763,6 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
   if (c->tile) {
     if (++c->epoch >= EPOCH_MAX) {  // granule epochs wrap: start clean
       GH_HIP(hipMemsetAsync(c->d_gran, 0, 8ull * c->gran_words, st));
-      if (c->d_tile_cnt) GH_HIP(hipMemsetAsync(c->d_tile_cnt, 0, 8ull * (c->tile_nrounds + 4), st));
       c->epoch = 1;
     }
     chain_lock.lock();
@@ -830,9 +845,6 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     t.stage_bytes = c->stage_bytes;
     t.junk = c->d_tile_junk;
     t.stamps = c->d_stamps;
-    t.tcnt = c->d_tile_cnt;
-    t.scratch = c->d_tile_scratch;
-    t.nrounds = c->tile_nrounds;
     const void* kern = tile_kernel_for(c->tile_minl, c->tile_g);
     if (c->ftile) {
       t.lut = c->d_ws_lut_c;

@@ -67,9 +67,6 @@ constexpr int TILE_SCAP = GH_TILE_SCAPB;  // staging bytes per segment (larger t
 #ifndef GH_TILE_PHI
 #define GH_TILE_PHI 2
 #endif
-#ifndef GH_TILE_DYN
-#define GH_TILE_DYN 0  // tiles handed out by per-round tickets (at most 2 per round per workgroup)
-#endif
 #ifndef GH_TILE_ALTPRIO
 #define GH_TILE_ALTPRIO 0
 #endif
@@ -151,12 +148,6 @@ struct TileParams {
   unsigned int kw, lutw_off, lutw_bytes;  // its width, LDS offset (a multiple of 8 << kw), bytes
   unsigned int stage_off;        // LDS offset of the staging
   unsigned int last_end;         // end bit of the stream's last segment when the shard holds it (else 0)
-  // GH_TILE_DYN builds: per-round ticket counters [2 parities][nrounds + 4] (this launch
-  // uses parity epoch & 1; the leader zeroes the other for the next launch), and
-  // per-workgroup scratch for tiles larger than the staging ([grid][2][TB][U][OW + 2])
-  unsigned int* tcnt;
-  uint32_t* scratch;
-  unsigned int nrounds;
 };
 
 // LDS of the tile kernel: LUT, two staging buffers, wave sums, leader wave totals.
@@ -564,8 +555,6 @@ __device__ __forceinline__ void tile_round_leader(const TileParams& p, uint32_t*
   const uint32_t A = (D + TB - 1) / TB;  // <= LEAD_A (the host caps the grid)
   const uint32_t nr = (p.ntiles + D - 1) / D;
   unsigned long long R = 0;
-  if (GH_TILE_DYN && p.tcnt)  // the next launch's ticket counters
-    for (uint32_t i = tid; i < p.nrounds + 4; i += TB) p.tcnt[((p.epoch + 1) & 1u) * (p.nrounds + 4) + i] = 0;
   for (uint32_t r = 0; r < nr; ++r) {
     const uint32_t t0 = r * D, n = min(D, p.ntiles - t0);
     uint32_t v[LEAD_A], sum = 0;
@@ -638,42 +627,9 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE,
   const uint32_t G = gridDim.x - 1, b = blockIdx.x - 1;  // decoding workgroups, this one
   const uint32_t nseg = (uint32_t)p.nseg;                 // < 2^31 (checked by the host)
   constexpr uint32_t NONE = 0xFFFFFFFFu;
-  // GH_TILE_DYN: tiles by ticket.  Round r = tiles [rG, rG + G) (the leader's rounds);
-  // a workgroup takes at most two tiles of a round, in increasing order, so a tile it
-  // waits for (two iterations back) never shares a round with a tile it holds
-  // unpublished (at most the two after it): no workgroup waits on itself, and a fast
-  // workgroup takes the tiles a slow one has not reached (static round robin made
-  // every round wait for the slowest workgroup).  Thread 0 takes the tickets; a ticket
-  // is requested at the top of an iteration and read after its decode.
-  uint32_t* s_tick = s_lead + NWAVE_T;  // [4] (in tile_lds_bytes' spare 32 bytes)
-  uint32_t r_cur = 0, n_cur = 0;         // thread 0: round of its newest ticket, tickets it took there
-  unsigned int* const tcnt = p.tcnt + (p.epoch & 1u) * (p.nrounds + 4);
-  // system scope (sc0 sc1): performed past the XCDs' L2s, so the eight XCDs' workgroups
-  // draw from one counter
-  auto tick_add = [](unsigned int* c) {
-    return __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  };
-  auto ticket_round = [&](bool same) { return n_cur == 0 ? 0u : (same && n_cur < 2) ? r_cur : r_cur + 1; };
-  auto ticket_done = [&](uint32_t rq, uint32_t x) -> uint32_t {  // thread 0: x = the counter's old value
-    for (;;) {
-      if (x < G && rq * G + x < p.ntiles) {
-        n_cur = (n_cur && rq == r_cur) ? n_cur + 1 : 1;
-        r_cur = rq;
-        return rq * G + x;
-      }
-      if (++rq >= p.nrounds) return NONE;
-      x = tick_add(tcnt + rq);  // (rare: the round was taken up)
-    }
-  };
-  if (GH_TILE_DYN && tid == 0) {
-    uint32_t rq = ticket_round(false);
-    s_tick[2] = ticket_done(rq, rq < p.nrounds ? tick_add(tcnt + rq) : G);
-    rq = ticket_round(false);
-    s_tick[3] = ticket_done(rq, rq < p.nrounds ? tick_add(tcnt + rq) : G);
-  }
   __syncthreads();
-  const uint32_t last_tile_k = GH_TILE_DYN ? p.ntiles + 4 : b < p.ntiles ? (p.ntiles - 1 - b) / G : NONE;
-  uint32_t cur = GH_TILE_DYN ? s_tick[2] : b, nxt = GH_TILE_DYN ? s_tick[3] : b + G;
+  const uint32_t last_tile_k = b < p.ntiles ? (p.ntiles - 1 - b) / G : NONE;
+  uint32_t cur = b, nxt = b + G;
   uint4 w[U];
   uint32_t w4[U], gw[U];
   auto load = [&](uint32_t t) {
@@ -697,7 +653,6 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE,
   if (cur >= p.ntiles) cur = NONE;
   uint32_t t1 = NONE, t2 = NONE;  // tiles of iterations k-1, k-2
   uint32_t tot1 = 0, tot2 = 0;    // their totals
-  bool sc1 = false, sc2 = false;  // (GH_TILE_DYN) they sit in the scratch, not the staging
   uint32_t buf = 0;               // k & 1
   bool ahead = false;             // the last prefix had to be polled
   unsigned long long gpc = 0;     // (IOVL) prefix of the next iteration's tile k-2, loaded early
@@ -727,11 +682,6 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE,
     } else {
       if (ahead) __builtin_amdgcn_s_setprio(GH_TILE_PLO);
       else __builtin_amdgcn_s_setprio(GH_TILE_PHI);
-    }
-    uint32_t tq_r = 0, tq_x = 0;  // (GH_TILE_DYN, thread 0) this iteration's ticket request
-    if (GH_TILE_DYN && tid == 0) {
-      tq_r = ticket_round(ahead);  // a workgroup that waited takes a second tile of its round
-      tq_x = tq_r < p.nrounds ? tick_add(tcnt + tq_r) : G;
     }
     // prefix of tile k-2 (lane 0 of every wave): loaded mid-decode (a load issued at the
     // top often saw the value a little before it was published, and the re-poll then
@@ -861,7 +811,6 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE,
 #pragma unroll
     for (int u = 0; u < U; ++u) bpos[u] = incl[u] - cnt[u];
     TSTAMP(3);
-    if (GH_TILE_DYN && tid == 0) s_tick[par] = ticket_done(tq_r, tq_x);  // tile of iteration k+2
     // ---- copy tile k-2 out (its prefix was published about an iteration ago) ----------
     // (one call site of load(nxt), after the prefix check: with a call in each branch the
     // compiler hoisted the loads above the check, whose vmcnt(0) then waited for them)
@@ -873,24 +822,8 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE,
     // prefetched loads with a counted vmcnt at the top of the next iteration.
     if (!(GH_TILE_ABLATE & 8) && !GH_TILE_IOVL)
       copy_out_tile<TB, TILE_NS, !GH_TILE_NOTAIL>(p.out, p.lut_bytes + buf * p.stage_bytes, goff,
-                                                   GH_TILE_DYN && sc2 ? 0u : n2, tid,
+                                                   n2, tid,
                                                    p.junk + (unsigned long long)blockIdx.x * TB + tid);
-    if (GH_TILE_DYN && sc2 && have2) {
-      // (rare) tile k-2 was larger than the staging: its words, counts and offsets from
-      // the scratch (written by this thread), stored byte-exact at the prefix; then
-      // drained, so the common path keeps its counted vmcnt
-      if (n2) {
-        const uint32_t* sc = p.scratch + (((unsigned long long)blockIdx.x * 2 + buf) * TB + tid) * (U * (OW + 2));
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          uint32_t o2[OW];
-#pragma unroll
-          for (int i = 0; i < OW; ++i) o2[i] = sc[u * (OW + 2) + i];
-          store_direct(p.out, p.out_cap, goff + sc[u * (OW + 2) + OW + 1], o2, sc[u * (OW + 2) + OW]);
-        }
-      }
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-    }
     TSTAMP(5);
     __syncthreads();  // tile sums
     TSTAMP(6);
@@ -908,20 +841,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE,
     // typical tile, not the worst case: see tile_setup); a larger tile waits for its own
     // prefix here and stores its bytes straight from registers
     const bool staged = have_cur && tile_total + (uint32_t)(STAGE_PAD + 48) <= p.stage_bytes;
-    if (GH_TILE_DYN && have_cur && !staged) {
-      // (rare) to the scratch, copied out two iterations later like a staged tile: a
-      // workgroup must not wait for its own tile's prefix here (its next tile may share
-      // the round)
-      uint32_t* sc = p.scratch + (((unsigned long long)blockIdx.x * 2 + buf) * TB + tid) * (U * (OW + 2));
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-#pragma unroll
-        for (int i = 0; i < OW; ++i) sc[u * (OW + 2) + i] = ow[u][i];
-        sc[u * (OW + 2) + OW] = cnt[u];
-        sc[u * (OW + 2) + OW + 1] = bpos[u];
-      }
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-    } else if (have_cur && !staged) {
+    if (have_cur && !staged) {
       unsigned long long goff = 0;
       bool got = true;
       if (lane == 0) {
@@ -974,12 +894,10 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE,
 #endif
     t2 = t1;
     tot2 = tot1;
-    sc2 = sc1;
-    t1 = (staged || (GH_TILE_DYN && have_cur)) ? cur : NONE;
-    sc1 = GH_TILE_DYN && have_cur && !staged;
+    t1 = staged ? cur : NONE;
     tot1 = tile_total;
     buf ^= 1u;
     cur = nxt < p.ntiles ? nxt : NONE;
-    nxt = GH_TILE_DYN ? s_tick[par] : nxt + G;
+    nxt += G;
   }
 }
