@@ -4,6 +4,7 @@
 # MI355X_MICROARCH.md "HBM"), summed over the kernels of one decode and averaged
 # over the traced decodes.
 # Usage: python scripts/pmc_traffic.py <out.json> <workload>=<fetch_dir>,<write_dir> ...
+# (env PMC_CMD: the profiled command, for the record; default the bench.py line)
 import csv, glob, json, os, sys, collections
 
 out_path = sys.argv[1]
@@ -36,7 +37,8 @@ for arg in sys.argv[2:]:
         "kernels": sorted(per["FETCH_SIZE"]),
         "source": f"{fdir.rstrip('/')}+{os.path.basename(wdir.rstrip('/'))}: "
                   "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of "
-                  f"`python3 bench.py --workload {wl.split('_')[0]} --cpu-sample 0 --no-copy`; "
+                  + os.environ.get("PMC_CMD", f"`python3 bench.py --workload {wl.split('_')[0]} --cpu-sample 0 --no-copy`")
+                  + "; "
                   "bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024 "
                   "per decode, summed over its kernels (gfx950 FETCH_SIZE halves wide streaming reads)",
     }
