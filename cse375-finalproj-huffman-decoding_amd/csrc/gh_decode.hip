@@ -374,37 +374,9 @@ static int ws_ns_for(double avg_seg_bytes) {
   return ns <= 2 ? 2 : ns <= 3 ? 3 : ns <= 4 ? 4 : ns <= 6 ? 6 : 8;
 }
 
-// Codes that take the canonical fallback anyway (longer than 12 bits, or incomplete):
-// the write LUT may be narrower than maxlen.  GH_WS_FBOCC=1 picks the widest width >= 8
-// whose LUT leaves room for one more write workgroup per CU (one chain's worst-case
-// staging per wave): long-code streams of one-bit codewords otherwise run one workgroup
-// per CU behind a 32 KB table.
-static uint32_t ws_fb_write_bits(const Canon& cn, uint32_t K, double avg_seg_bytes) {
-  const char* e = getenv("GH_WS_FBOCC");
-  if (!e || atoi(e) == 0 || getenv("GH_WS_K")) return K;
-  const uint32_t maxsyms = std::min<uint32_t>(143 / std::max<uint32_t>(cn.minlen, 1) + 1, 255);
-  const size_t chain_worst = 64ull * maxsyms + 64;
-  const size_t typical = (size_t)(1.3 * avg_seg_bytes * 64 * WS_U) + 64;
-  const size_t want = std::max(chain_worst, std::min<size_t>(64ull * WS_U * maxsyms + 64, typical));
-  constexpr int NW = WS_TB / 64;
-  auto wgs = [&](uint32_t k, size_t need) {
-    const long lb = (long)(8ull << k) + (long)FB_BYTES;
-    int best = 0;
-    for (int wg = 8; wg >= 1 && !best; --wg)
-      if (((long)(163840 / wg) - lb) / NW >= (long)need) best = wg;
-    return best;
-  };
-  const int base = std::max(wgs(K, want), wgs(K, chain_worst));
-  for (uint32_t k = K; k >= 8; --k)
-    if (wgs(k, chain_worst) > base) return k;
-  return K;
-}
-
 static int ws_setup(gh_ctx* c, double avg_seg_bytes) {
   const Canon& cn = c->canon;
-  const uint32_t kc = ws_count_bits(cn);
-  uint32_t K = ws_write_bits(cn);
-  if (kraft16(cn) != 65536 || cn.maxlen > std::min(K, kc)) K = ws_fb_write_bits(cn, K, avg_seg_bytes);
+  const uint32_t K = ws_write_bits(cn), kc = ws_count_bits(cn);
   // canonical fallback: codewords longer than a table, or patterns outside an incomplete
   // code (a LUT entry with no codeword)
   const bool fb = kraft16(cn) != 65536 || cn.maxlen > std::min(K, kc);
