@@ -125,6 +125,21 @@ def test_gpu_sync_gaps_match_oracle(gpu, orc, r, n):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n", [200, 270, 290, 16_720, 16_740, 16_760, 33_440, 33_460, 49_100])
+def test_gpu_sync_block_and_wave_edges(gpu, orc, n):
+    """r = 0.1 streams (~16 symbols per segment) whose segment counts fall around the
+    walk kernel's block (16 segments per lane) and wave (1024 segments) edges: a last
+    block shorter than 16 segments, exactly 16, 17 (g = 11, 16, 17, 1023, 1024, 1025,
+    2048, 2049, 3008): a wave with one lane, the fix pass's wave starts."""
+    d = orc.generate(11, 0.1, n)
+    syms = orc.symbols_of(d)
+    units = orc.raw_encode(d, syms)
+    gaps, rep = _sync_on_gpu(gpu, units, syms)
+    assert np.array_equal(gaps, orc.raw_gaps(d, syms))
+    assert np.array_equal(gpu.decode_raw(units, syms, d.size), d)
+
+
+@pytest.mark.gpu
 def test_gpu_sync_long_codes(gpu, orc):
     """Codes longer than the 13-bit sync LUT (SK = 13, gh_sync.hip: the LONG kernels'
     canonical-threshold path), up to 16 bits, from the geometric fixture."""
