@@ -67,9 +67,6 @@ constexpr int TILE_SCAP = GH_TILE_SCAPB;  // staging bytes per segment (larger t
 #ifndef GH_TILE_PHI
 #define GH_TILE_PHI 2
 #endif
-#ifndef GH_TILE_WEIGHT
-#define GH_TILE_WEIGHT 0  // rounds per weighting period (0: plain static round robin)
-#endif
 #ifndef GH_TILE_ALTPRIO
 #define GH_TILE_ALTPRIO 0
 #endif
@@ -631,26 +628,8 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE,
   const uint32_t nseg = (uint32_t)p.nseg;                 // < 2^31 (checked by the host)
   constexpr uint32_t NONE = 0xFFFFFFFFu;
   __syncthreads();
-  // GH_TILE_WEIGHT = P > 1: in every P rounds, the last round's tiles of the workgroups
-  // dispatched second on their CU (decoding index >= G - NF, measured ~5 % slower) go to
-  // the first-dispatched ones (index < NF) as a second tile of that round: at most two
-  // tiles of a round per workgroup, in increasing order, so the round leader stays
-  // deadlock-free (a workgroup never waits on a round it holds an unpublished tile of).
-  constexpr uint32_t WP = GH_TILE_WEIGHT;
-  const uint32_t NF = G / 2;
-  auto tile_of = [&](uint32_t k) -> uint32_t {
-    if (WP < 2) return b + k * G;
-    const bool fast = b < NF, slow = b >= G - NF;
-    const uint32_t per = fast ? WP + 1 : slow ? WP - 1 : WP;
-    const uint32_t sr = k / per, j = k % per;
-    const unsigned long long base = (unsigned long long)sr * WP * G;
-    const unsigned long long t = j < WP ? base + (unsigned long long)j * G + b  // (slow: j < WP - 1)
-                                        : base + (unsigned long long)(WP - 1) * G + b + (G - NF);
-    return t < p.ntiles ? (uint32_t)t : NONE;
-  };
-  const uint32_t last_tile_k = WP < 2 ? (b < p.ntiles ? (p.ntiles - 1 - b) / G : NONE)
-                                      : (p.ntiles / G + 2) * (WP + 1) / (WP - 1) + 2;
-  uint32_t cur = tile_of(0), nxt = tile_of(1);
+  const uint32_t last_tile_k = b < p.ntiles ? (p.ntiles - 1 - b) / G : NONE;
+  uint32_t cur = b, nxt = b + G;
   uint4 w[U];
   uint32_t w4[U], gw[U];
   auto load = [&](uint32_t t) {
@@ -919,6 +898,6 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE,
     tot1 = tile_total;
     buf ^= 1u;
     cur = nxt < p.ntiles ? nxt : NONE;
-    nxt = WP < 2 ? nxt + G : tile_of(k + 2);
+    nxt += G;
   }
 }
