@@ -127,6 +127,9 @@ __device__ __forceinline__ uint32_t enc_block_scan(uint32_t x, uint32_t* s_red, 
 // group's bytes (EBQ 16-byte loads per thread: the bytes in flight per CU set this
 // kernel's bandwidth) are loaded before the current group's reduction.  Loads are
 // unconditional (chunk index clamped, input padded past n), bytes past n masked by index.
+#ifndef GH_ENC_NT
+#define GH_ENC_NT 3  // (round 4: 3) write kernel, bits: 1 input loads nontemporal, 2 payload word stores nontemporal; 4 bits-kernel loads nontemporal
+#endif
 #ifndef GH_ENC_BQ
 #define GH_ENC_BQ 2  // chunks in flight per thread (4 measured slower: 246 vs 229 us on cfg4)
 #endif
@@ -139,7 +142,13 @@ __global__ __launch_bounds__(ETB) void gh_enc_bits_kernel(const uint8_t* in, uin
   for (int i = tid; i < 256; i += ETB) s_len[i] = lut[i] & 0xFFu;
   const uint32_t G = gridDim.x;
   auto ld = [&](uint32_t cc) {
-    return *(const uint4*)(in + (uint64_t)min(cc, nchunks - 1) * ECHUNK + (uint64_t)tid * EBPT);
+    const uint8_t* src = in + (uint64_t)min(cc, nchunks - 1) * ECHUNK + (uint64_t)tid * EBPT;
+    if (GH_ENC_NT & 4) {
+      typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+      const v4u t = __builtin_nontemporal_load((const v4u*)src);
+      return make_uint4(t.x, t.y, t.z, t.w);
+    }
+    return *(const uint4*)src;
   };
   auto chunk_bits_of = [&](const uint4& v, uint32_t cc) {
     const uint64_t ib = (uint64_t)cc * ECHUNK + (uint64_t)tid * EBPT;
@@ -292,7 +301,13 @@ __global__ __launch_bounds__(ETB) __attribute__((amdgpu_waves_per_eu(6))) void g
   // bytes past n; bytes past n are masked by index), so no branch holds a load
   auto fetch = [&](uint32_t cc) {
     const uint64_t ib = (uint64_t)cc * ECHUNK + (uint64_t)tid * EBPT;
-    v = *(const uint4*)(p.in + ib);
+    if (GH_ENC_NT & 1) {
+      typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+      const v4u t = __builtin_nontemporal_load((const v4u*)(p.in + ib));
+      v = make_uint4(t.x, t.y, t.z, t.w);
+    } else {
+      v = *(const uint4*)(p.in + ib);
+    }
     offb = p.blk_off[cc / SCAN_BLK];
     offl = p.chunk_loc[cc];
     xbyte = p.in[(uint64_t)(cc + 1) * ECHUNK + (uint64_t)(lane & 31)];  // the next chunk's byte lane & 31
@@ -408,7 +423,9 @@ __global__ __launch_bounds__(ETB) __attribute__((amdgpu_waves_per_eu(6))) void g
       const uint32_t i = (uint32_t)tid + (uint32_t)(ETB * j);
       const uint32_t x = s_w[i < (uint32_t)EWORDS ? i : 0u];
       if (i <= w1) s_w[i] = 0;
-      *((i >= w0 && i < w1) ? wout + i : junk) = x;
+      uint32_t* d = (i >= w0 && i < w1) ? wout + i : junk;
+      if (GH_ENC_NT & 2) __builtin_nontemporal_store(x, d);
+      else *d = x;
     }
     for (uint32_t i = tid + ETB * NSW; i <= w1; i += ETB) {
       const uint32_t x = s_w[i];

@@ -121,6 +121,22 @@ constexpr int TILE_SCAP = GH_TILE_SCAPB;  // staging bytes per segment (larger t
 #ifndef GH_TILE_TRIM
 #define GH_TILE_TRIM 1  // stop shifting window words no kept codeword can still read
 #endif
+#ifndef GH_TILE_NT
+#define GH_TILE_NT 2  // bits: 1 payload loads nontemporal, 2 copy-out 16-byte stores nontemporal (round 4: 2)
+#endif
+typedef unsigned int tile_v4u __attribute__((ext_vector_type(4)));
+// 16-byte global store of the copy-out (GH_TILE_NT & 2: streaming, the output is not re-read)
+__device__ __forceinline__ void tile_st16(uint4* d, const uint4& v) {
+  if (GH_TILE_NT & 2) __builtin_nontemporal_store(tile_v4u{v.x, v.y, v.z, v.w}, (tile_v4u*)d);
+  else *d = v;
+}
+__device__ __forceinline__ uint4 tile_ld16(const uint32_t* s) {
+  if (GH_TILE_NT & 1) {
+    const tile_v4u v = __builtin_nontemporal_load((const tile_v4u*)s);
+    return make_uint4(v.x, v.y, v.z, v.w);
+  }
+  return *(const uint4*)s;
+}
 constexpr int TILE_MIDG = GH_TILE_MIDG;  // decode group after which the mid-decode loads are issued
 constexpr int STAGE_PAD = 16;      // staging byte STAGE_PAD + i = tile byte i
 // Output words per segment: a segment holds at most ceil(128 / minlen) codewords (8
@@ -403,10 +419,10 @@ __device__ __forceinline__ void copy_out_tile(uint8_t* out, uint32_t stg, unsign
       const bool real = c < ce;
       const uint32_t cs = real ? c : ce - 1u;
       const uint4 v = lds_u128(src + 16u * ((real || have) ? cs : cf));
-      *((real || have) ? (uint4*)(o + 16ull * cs) : junk) = v;
+      tile_st16((real || have) ? (uint4*)(o + 16ull * cs) : junk, v);
     }
     for (uint32_t c = cf + (uint32_t)tid + (uint32_t)(TBK * NS); c < ce; c += TBK)
-      *(uint4*)(o + 16ull * c) = lds_u128(src + 16u * c);
+      tile_st16((uint4*)(o + 16ull * c), lds_u128(src + 16u * c));
   } else {
     // NS x TBK chunks cover every staged tile (the host sizes NS): no loop, so the
     // store count is fixed and the next iteration's wait for its prefetched loads
@@ -418,7 +434,7 @@ __device__ __forceinline__ void copy_out_tile(uint8_t* out, uint32_t stg, unsign
     const uint32_t cs0 = real0 ? c0 : (have ? ce - 1u : cf);
     const uint4 v0 = lds_u128(src + 16u * cs0);
     uint4* const d0 = (real0 || have) ? (uint4*)(o + 16ull * cs0) : junk;
-    *d0 = v0;
+    tile_st16(d0, v0);
 #pragma unroll
     for (int i = 1; i < NS; ++i) {
       const uint32_t c = c0 + (uint32_t)(TBK * i);
@@ -428,7 +444,7 @@ __device__ __forceinline__ void copy_out_tile(uint8_t* out, uint32_t stg, unsign
         v = lds_u128(src + 16u * c);
         d = (uint4*)(o + 16ull * c);
       }
-      *d = v;
+      tile_st16(d, v);
     }
   }
   // edge bytes: the head chunk's [lb, min(16, lb + n)) when lb != 0, then the tail
@@ -637,7 +653,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE,
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t sc = min(seg0 + (uint32_t)(u * TB), nseg - 1);
-      w[u] = *(const uint4*)(p.payload + 4ull * sc);
+      w[u] = tile_ld16(p.payload + 4ull * sc);
       w4[u] = p.payload[4ull * sc + 4];
       gw[u] = p.gaps[(p.gap_nib0 + (sc ? sc - 1u : 0u)) >> 3];
     }

@@ -96,6 +96,22 @@ struct WsParams {
 #define WS_CK(cond, bit) true
 #endif
 
+#ifndef GH_WS_NT
+#define GH_WS_NT 3  // (round 4: 3) bits: 1 payload loads nontemporal (both kernels), 2 write-kernel 16-byte stores nontemporal
+#endif
+typedef unsigned int ws_v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void ws_st16(uint4* d, const uint4& v) {
+  if (GH_WS_NT & 2) __builtin_nontemporal_store(ws_v4u{v.x, v.y, v.z, v.w}, (ws_v4u*)d);
+  else *d = v;
+}
+__device__ __forceinline__ uint4 ws_ld16(const uint32_t* s) {
+  if (GH_WS_NT & 1) {
+    const ws_v4u v = __builtin_nontemporal_load((const ws_v4u*)s);
+    return make_uint4(v.x, v.y, v.z, v.w);
+  }
+  return *(const uint4*)s;
+}
+
 // Blocks [b0, b1) of 64*U segments of range r (ranges are cut at superblock edges, so
 // kernels with different U cover the same segments).
 template <int U>
@@ -117,7 +133,7 @@ __device__ __forceinline__ void ws_load(const WsParams& p, uint32_t blk, int lan
     const uint32_t seg = blk * (uint32_t)(64 * U) + (uint32_t)(64 * u + lane);
     const uint32_t sc = min(seg, p.nseg - 1);
     if (WS_CK(4ull * sc + 5 <= p.chk_pay || !GH_WS_CHECK, 0x100)) {
-      w[u] = *(const uint4*)(p.payload + 4ull * sc);
+      w[u] = ws_ld16(p.payload + 4ull * sc);
       w4[u] = p.payload[4ull * sc + 4];
     }
     if (WS_CK(((p.gap_nib0 + sc) >> 3) < p.chk_gap || !GH_WS_CHECK, 0x200)) {
@@ -508,11 +524,11 @@ __global__ __launch_bounds__(TBK) void gh_ws_write_kernel(const WsParams p) {
             const uint32_t cs = real ? c : cdup;
             const uint4 d = st4[cs];
             uint4* dst = (real || have) ? (uint4*)(p.out + a0 - 16 + 16ull * cs) : junk;
-            if (WS_CK(!real || a0 + 16ull * c <= p.chk_out || !GH_WS_CHECK, 0x2000)) *dst = d;
+            if (WS_CK(!real || a0 + 16ull * c <= p.chk_out || !GH_WS_CHECK, 0x2000)) ws_st16(dst, d);
           }
           for (uint32_t c = c_lo + (uint32_t)lane + 64u * NS; c < cend; c += 64u)
             if (WS_CK(a0 + 16ull * c <= p.chk_out || !GH_WS_CHECK, 0x4000))
-              *(uint4*)(p.out + a0 - 16 + 16ull * c) = st4[c];
+              ws_st16((uint4*)(p.out + a0 - 16 + 16ull * c), st4[c]);
         }
         if (goff + hbytes >= p.out_cap) {
           // the output ends in this piece: its partial last chunk (staging chunk cend,

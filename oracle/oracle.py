@@ -269,14 +269,17 @@ def raw_encode(data, syms) -> np.ndarray:
 
 def raw_gaps(data, syms) -> np.ndarray:
     """Gap words of the raw stream: entry of segment j+1 (first codeword start at
-    or after 128(j+1)) minus 128(j+1) in nibble j, 8 per u32 LSB-first; the last
-    nibble is 0 (encoder.cu:307-312,358-379)."""
+    or after 128(j+1), or the end of the last codeword when it crosses 128(j+1))
+    minus 128(j+1) in nibble j, 8 per u32 LSB-first; the last nibble is 0
+    (encoder.cu:307-312,358-379)."""
     d, _, l = _code_arrays(data, syms)
     bits = int(l.sum())
     g = ((bits + 31) // 32 + 3) // 4
     nib = np.zeros(8 * ((g + 7) // 8), dtype=np.uint32)
     if g > 1:
-        starts = np.cumsum(l) - l
+        # codeword starts plus the stream's end: a boundary crossed by the LAST codeword
+        # gets that codeword's end, as encoder.cu:307-312 records every crossing codeword
+        starts = np.append(np.cumsum(l) - l, bits)
         bnd = 128 * np.arange(1, g, dtype=np.uint64)
         idx = np.searchsorted(starts, bnd)
         entry = np.where(idx < starts.size, starts[np.minimum(idx, starts.size - 1)], bnd)

@@ -80,6 +80,19 @@ def test_raw_stream_is_gap_array_payload(orc, gh, r, n):
     assert np.array_equal(orc.raw_encode(d, s.symbols), pw)
 
 
+@pytest.mark.parametrize("n", [200, 270, 290])
+def test_raw_gaps_last_codeword_crossing(orc, gh, n):
+    """r = 0.1, seed 11: at n = 270 the stream's last codeword crosses the boundary
+    128 (g - 1) and ends 2 bits past it; the gap-array encoder records that end
+    (encoder.cu:307-312), and so must the raw stream's gap words."""
+    import ctypes
+    d = orc.generate(11, 0.1, n)
+    s = gh.parse(orc.encode(d))
+    nw = (s.g + 7) // 8
+    gw = np.ctypeslib.as_array(ctypes.cast(s.c.gap_words, ctypes.POINTER(ctypes.c_uint32)), (max(nw, 1),))[:nw]
+    assert np.array_equal(orc.raw_gaps(d, s.symbols), gw)
+
+
 def test_desync_table_oracle(orc):
     """The adversarial stream of the GPU repair test: a 1-bit code plus four 3-bit
     codes, data all '111' — a walk that starts off the 3-bit phase never resyncs."""
