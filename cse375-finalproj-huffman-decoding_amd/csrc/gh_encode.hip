@@ -133,13 +133,18 @@ __device__ __forceinline__ uint32_t enc_block_scan(uint32_t x, uint32_t* s_red, 
 #ifndef GH_ENC_BQ
 #define GH_ENC_BQ 2  // chunks in flight per thread (4 measured slower: 246 vs 229 us on cfg4)
 #endif
+#ifndef GH_ENC_BREP
+#define GH_ENC_BREP 32  // code-length table copies in LDS (lane l reads copy l mod BREP: no bank conflicts at 32)
+#endif
 constexpr int EBQ = GH_ENC_BQ;
+constexpr int EBREP = GH_ENC_BREP;
 __global__ __launch_bounds__(ETB) void gh_enc_bits_kernel(const uint8_t* in, uint64_t n, uint32_t nchunks,
                                                           const uint32_t* lut, uint32_t* chunk_bits) {
-  __shared__ uint32_t s_len[256];
+  __shared__ uint32_t s_lenr[256 * EBREP];
   __shared__ uint32_t s_red[2][EBQ][ETB / 64];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  for (int i = tid; i < 256; i += ETB) s_len[i] = lut[i] & 0xFFu;
+  for (int i = tid; i < 256 * EBREP; i += ETB) s_lenr[i] = lut[i / EBREP] & 0xFFu;
+  const uint32_t* s_len = s_lenr + (lane & (EBREP - 1));  // entry b of this lane's copy: s_len[b * EBREP]
   const uint32_t G = gridDim.x;
   auto ld = [&](uint32_t cc) {
     const uint8_t* src = in + (uint64_t)min(cc, nchunks - 1) * ECHUNK + (uint64_t)tid * EBPT;
@@ -155,11 +160,11 @@ __global__ __launch_bounds__(ETB) void gh_enc_bits_kernel(const uint8_t* in, uin
     uint32_t bits = 0;
     if (ib + EBPT <= n) {
 #pragma unroll
-      for (int k = 0; k < EBPT; ++k) bits += s_len[enc_byte(v, k)];
+      for (int k = 0; k < EBPT; ++k) bits += s_len[enc_byte(v, k) * EBREP];
     } else {
       const uint32_t rem = ib < n ? (uint32_t)(n - ib) : 0u;
 #pragma unroll
-      for (int k = 0; k < EBPT; ++k) bits += (uint32_t)k < rem ? s_len[enc_byte(v, k)] : 0u;
+      for (int k = 0; k < EBPT; ++k) bits += (uint32_t)k < rem ? s_len[enc_byte(v, k) * EBREP] : 0u;
     }
     return bits;
   };
@@ -263,7 +268,15 @@ struct EncParams {
   uint32_t nchunks;
 };
 
-constexpr int ELREP = 16;  // write-kernel LUT replicas (lane & 15): a lookup collides at most 2-way
+// Write-kernel LUT replicas (lane l reads copy l mod ELREP): 16 copies collide at most
+// 2-way and leave room for 6 waves per SIMD; the long-code shapes (NSW >= 6: cfg4's
+// r = 0.1 codes, ~8 bits per byte) take 32 (conflict-free, 3 workgroups per CU by LDS):
+// cfg4 1.055 vs 1.096 ms, while cfg3 / cfg2 lose 6-11 % at 32 (round 4, gpurun_out/r04x).
+#ifndef GH_ENC_LREP_LONG
+#define GH_ENC_LREP_LONG 32
+#endif
+template <int NSW>
+constexpr int enc_lrep() { return NSW >= 6 ? GH_ENC_LREP_LONG : 16; }
 
 // A thread's 16 codewords, combined in registers: LUT entries hold the code
 // left-aligned, e = code << (32 - len) | len (len <= 16 sits in the low 5 bits, below
@@ -284,7 +297,9 @@ __device__ __forceinline__ uint32_t enc_pair(uint32_t a, uint32_t c, uint32_t& l
 // than the prefetch the next chunk waits for its loads with vmcnt(N) instead of also
 // waiting for this chunk's stores.
 template <int NSW>
-__global__ __launch_bounds__(ETB) __attribute__((amdgpu_waves_per_eu(6))) void gh_enc_write_kernel(const EncParams p) {
+__global__ __launch_bounds__(ETB) __attribute__((amdgpu_waves_per_eu(enc_lrep<NSW>() > 16 ? 3 : 6))) void gh_enc_write_kernel(
+    const EncParams p) {
+  constexpr int ELREP = enc_lrep<NSW>();
   __shared__ uint32_t s_lutr[257 * ELREP];  // left-aligned entries, replicated
   __shared__ uint32_t s_w[EWORDS];
   __shared__ uint32_t s_g[EGAPW];
