@@ -6,7 +6,7 @@
 #           cfg3 / cfg2 bench lines;
 #   part b: rocprofv3 kernel stats per workload, FETCH_SIZE / WRITE_SIZE passes
 #           (-> pmc_traffic.json), SQ passes of the cfg4 tile kernel;
-#   part c: GPU encoder, self-sync, long codes, shard concurrency.
+#   part c: GPU encoder, self-sync, long codes, shard concurrency (bc: b then c).
 set -o pipefail
 cd "$(dirname "$0")/.." || exit 1
 R=${R:-r04}
@@ -23,4 +23,6 @@ case ${1:-a} in
     bash scripts/lease.sh "$O" "cmd encode 300 python -u scripts/bench_encode.py" \
       "cmd sync 300 python -u scripts/bench_sync.py" "cmd longcodes 500 python -u scripts/time_longcodes.py" \
       "cmd shards 300 python -u scripts/bench_shards.py" ;;
+  bc)
+    bash scripts/round_gpu.sh b && bash scripts/round_gpu.sh c ;;
 esac
