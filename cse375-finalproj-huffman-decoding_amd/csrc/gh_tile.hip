@@ -137,6 +137,10 @@ __device__ __forceinline__ uint4 tile_ld16(const uint32_t* s) {
   }
   return *(const uint4*)s;
 }
+#ifndef GH_TILE_W4DPP
+#define GH_TILE_W4DPP 0  // look-ahead dword from the next lane (DPP wave_shl:1); lane 63 and the
+                         // shard's last segment from one wave-uniform load
+#endif
 constexpr int TILE_MIDG = GH_TILE_MIDG;  // decode group after which the mid-decode loads are issued
 constexpr int STAGE_PAD = 16;      // staging byte STAGE_PAD + i = tile byte i
 // Output words per segment: a segment holds at most ceil(128 / minlen) codewords (8
@@ -654,7 +658,12 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE,
     for (int u = 0; u < U; ++u) {
       const uint32_t sc = min(seg0 + (uint32_t)(u * TB), nseg - 1);
       w[u] = tile_ld16(p.payload + 4ull * sc);
-      w4[u] = p.payload[4ull * sc + 4];
+      if (GH_TILE_W4DPP) {  // lane 63's look-ahead (every lane the same address)
+        const uint32_t s63 = min(seg0 - (uint32_t)lane + 63u + (uint32_t)(u * TB), nseg - 1);
+        w4[u] = p.payload[4ull * s63 + 4];
+      } else {
+        w4[u] = p.payload[4ull * sc + 4];
+      }
       gw[u] = p.gaps[(p.gap_nib0 + (sc ? sc - 1u : 0u)) >> 3];
     }
   };
@@ -779,7 +788,15 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE,
         const uint32_t seg = seg0 + (uint32_t)(u * TB);
         act[u] = have_cur && seg < nseg;
         start[u] = seg == 0 ? (int)p.first_start : (int)gap_nib(gw[u], p.gap_nib0 + seg - 1u);
-        make_ewin(w[u], w4[u], start[u], S, e[u]);
+        uint32_t la = w4[u];
+        if (GH_TILE_W4DPP) {
+          // segment seg + 1's first dword is the next lane's w.x (wave_shl:1; lane 63 keeps
+          // the uniform load, and so does the shard's last segment, whose look-ahead is
+          // the zero padding past it)
+          const uint32_t nx = (uint32_t)__builtin_amdgcn_update_dpp((int)w4[u], (int)w[u].x, 0x130, 0xf, 0xf, false);
+          la = (lane == 63 || seg + 1u >= nseg) ? w4[u] : nx;
+        }
+        make_ewin(w[u], la, start[u], S, e[u]);
       }
       TSTAMP(1);
       // GH_TILE_EARLY: the next tile's loads right here, into the registers the windows
