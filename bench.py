@@ -498,8 +498,11 @@ def main() -> int:
             "gather_ms": None if res["gather_ms"] is None else round(res["gather_ms"], 3),
             "gather_bitexact": res["gather_ok"],
             "load_ms": round(res["load_ms"], 2),
-            "load_kind": "host memory -> HBM (pageable)" if not use_dist else
-                         f"gh_ctx_load_file: {res['share_dir']} file -> pinned -> HBM, shard words only",
+            "load_kind": (("host memory -> HBM (pageable)" if os.environ.get("GH_H2D") == "pageable"
+                           or res.get("load_bytes", 1 << 30) < (8 << 20) else
+                           "host memory -> pinned double-buffered staging -> HBM (the first load "
+                           "of a process also pins the staging set)") if not use_dist else
+                         f"gh_ctx_load_file: {res['share_dir']} file -> pinned -> HBM, shard words only"),
             "dist": {"backend": "nccl (RCCL)", "world": world, "forced": bool(args.force_dist and world == 1),
                      "share_dir": res["share_dir"]} if use_dist else None,
             "e2e": e2e,

@@ -119,6 +119,9 @@ struct StagingLease {
     return s->init();
   }
   ~StagingLease() {
+    // an error return may leave copies of this call in flight: drain them before the
+    // caller frees their buffers or the set goes back to the pool
+    if (s && s->st) (void)hipStreamSynchronize(s->st);
     {
       std::lock_guard<std::mutex> g(g_pool_mu);
       if (counted) --g_live[dev];

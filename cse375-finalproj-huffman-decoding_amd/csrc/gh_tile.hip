@@ -1,13 +1,14 @@
-// Tile kernel: the decode of grouped codes (complete, 4 <= len <= 12, e.g. BASELINE's
-// r = 0.1 data), included by gh_decode.hip.  Reference counterpart: gpu_dec_l1_l2
-// (decoder/src/decoder.cu:454-730) — its per-segment count (:529-569), decoupled
-// look-back (:571-653) and second decode that writes the bytes (:655-728) — as ONE
-// decode pass per segment in one persistent kernel.
+// Tile kernel: the decode of grouped codes (complete, 3 <= len <= 12, e.g. BASELINE's
+// r = 0.1 and r = 0.5 data), included by gh_decode.hip.  Reference counterpart:
+// gpu_dec_l1_l2 (decoder/src/decoder.cu:454-730) — its per-segment count (:529-569),
+// decoupled look-back (:571-653) and second decode that writes the bytes (:655-728) — as
+// ONE decode pass per segment in one persistent kernel.
 //
-// 512-thread workgroups, three segments per lane, a tile = 1536 consecutive segments.
-// Workgroup 0 is the round leader; the D = grid - 1 others decode: workgroup b takes
-// tiles b, b + D, b + 2D, ... (static round robin; grid <= 2048).  Iteration k of a
-// decoding workgroup:
+// 512-thread workgroups, U segments per lane, a tile = U * 512 consecutive segments; wave
+// w of a workgroup owns the 64 * U consecutive segments [64Uw, 64U(w+1)) of its tile, lane
+// l of chain u the segment 64Uw + 64u + l.  Workgroup 0 is the round leader; the
+// D = grid - 1 others decode: workgroup b takes tiles b, b + D, b + 2D, ... (static round
+// robin; grid <= 2048).  Iteration k of a decoding workgroup:
 //
 //   decode tile k into registers (one codeword per lookup, G codewords per window shift;
 //     a codeword is kept iff it starts before the segment end: the reference's rule)
@@ -15,91 +16,35 @@
 //   copy tile k-2 out of staging (its prefix has had an iteration to arrive), with a
 //     fixed store count; the next tile's loads are issued just before
 //   wave scans of the counts -> BARRIER -> publish tile k's aggregate
-//   stage tile k (aligned dword stores, a second barrier, the 1-3 head bytes); a tile
-//     larger than staging (20 bytes per segment) waits for its prefix and stores its
-//     bytes straight from registers
+//   stage tile k: every wave writes its own 64U segments (no second barrier, below); a
+//     tile larger than staging waits for its prefix and stores its bytes from registers
 //
 // The leader takes the rounds (tiles rD .. rD + D - 1) in order: it waits for a round's
 // aggregates, scans them and publishes every tile's global exclusive prefix.  The start
 // of the next round stays in its registers, so the serial chain of round starts never
 // crosses workgroups (rotating the leader role among the decoding workgroups made every
-// round pay one cross-workgroup hand-off on that chain: 0.73 vs 0.70 ms on cfg4).  A
-// decoupled look-back with 512 tiles in flight needed a window of ~512 granules per tile
-// and mostly took its slow path.
+// round pay one cross-workgroup hand-off on that chain: 0.73 vs 0.70 ms on cfg4).
 //
 // Issue priority: the second workgroup dispatched to a CU loses issue-arbitration ties to
 // the first (age order), so one slot runs ~30 % slower and the other waits for its
 // prefixes.  A wave whose last prefix had to be polled is ahead of the grid and drops to
-// priority 0; one that found it published is behind and takes priority 2 (cfg4 0.70 ->
-// 0.68 ms; alternating the two slots' priority by iteration gave 0.747 -> 0.729 ms).
+// priority 0; one that found it published is behind and takes priority 2.
+//
+// Every alternative of the round-3/4 build knobs (copy-out interleaving, batched reads,
+// early loads, ticket schedules, priority rotations, ...) measured slower and was removed
+// (tile-kernel section).  Diagnostic builds only: GH_TILE_STAMPS, GH_TILE_ABLATE.
 
-// Build knobs (make variant VFLAGS=-D...; every alternative value is measured in
-// DESIGN.md's tile-kernel section, the defaults are the fastest).
 #ifndef GH_TILE_TB
-#define GH_TILE_TB 512
+#define GH_TILE_TB 1024
 #endif
 constexpr int TILE_TB = GH_TILE_TB;  // threads per workgroup
-#ifndef GH_TILE_U
-#define GH_TILE_U 3
-#endif
-#ifndef GH_TILE_NOTAIL
-#define GH_TILE_NOTAIL 0  // copy-out: NS = 4 fixed stores per thread, no loop for extra chunks
-#endif
-#if GH_TILE_NOTAIL
-#undef GH_TILE_NS
-#define GH_TILE_NS 4
-#endif
-#ifndef GH_TILE_NS
-#define GH_TILE_NS 2
-#endif
-#ifndef GH_TILE_WPE
-#define GH_TILE_WPE 4  // waves per SIMD the kernel is compiled for (2 workgroups per CU: 128 VGPRs)
-#endif
-constexpr int TILE_U = GH_TILE_U;    // segments per lane
-constexpr int TILE_NS = GH_TILE_NS;  // 16-byte stores per thread per copy-out (the rest of a tile loops)
-#ifndef GH_TILE_SCAPB
-#define GH_TILE_SCAPB 20
-#endif
-constexpr int TILE_SCAP = GH_TILE_SCAPB;  // staging bytes per segment (larger tiles bypass staging)
-#ifndef GH_TILE_MIDG
-#define GH_TILE_MIDG 2
-#endif
-#ifndef GH_TILE_PHI
-#define GH_TILE_PHI 2
-#endif
-#ifndef GH_TILE_ALTPRIO
-#define GH_TILE_ALTPRIO 0
-#endif
-#ifndef GH_TILE_PLO
-#define GH_TILE_PLO 0
-#endif
-#ifndef GH_POLL_SLEEP
-#define GH_POLL_SLEEP 2
-#endif
-#ifndef GH_TILE_NOZERO
-#define GH_TILE_NOZERO 1  // leave the decode's output words unzeroed (bytes past the count are never kept)
-#endif
-#ifndef GH_TILE_MERGEWAIT
-#define GH_TILE_MERGEWAIT 1
-#endif
-#ifndef GH_TILE_EARLY
-#define GH_TILE_EARLY 0  // issue the next tile's loads before the decode instead of before the copy-out
-#endif
-#ifndef GH_TILE_BATCH
-#define GH_TILE_BATCH 0  // copy-out: the thread's LDS reads issued together behind one wait
-#endif
-#ifndef GH_TILE_WPRIO
-#define GH_TILE_WPRIO 0  // waves 4-7 (the second wave on each SIMD) one issue priority level up
-#endif
-#ifndef GH_TILE_P1MIN
-#define GH_TILE_P1MIN 0  // staging phase 1: the first dwords every kept segment fills, unmasked
-#endif
-#ifndef GH_TILE_IOVL
-#define GH_TILE_IOVL 0  // copy-out parts between the decode groups of the next tile
-#endif
-#ifndef GH_TILE_IOB
-#define GH_TILE_IOB 2   // (IOVL) the decode group after which the prefix is checked
-#endif
+constexpr int TILE_U = 3;     // segments per lane, codes of >= 4-bit codewords
+constexpr int TILE_U3 = 2;    // segments per lane, codes with 3-bit codewords
+constexpr int TILE_NS = 4;    // 16-byte stores per lane per copy-out (NS * 64 chunks cover a wave's piece)
+constexpr int TILE_SCAP = 20; // staging bytes per segment, codes of >= 4-bit codewords
+constexpr int TILE_MIDG = 2;  // decode group after which the prefix of tile k-2 is loaded (again)
+constexpr int STAGE_PAD = 16; // region byte STAGE_PAD + i = piece byte i
+constexpr int TILE_SLOTS = 8; // per-tile wave totals / offsets / arrival counters in LDS, by k mod 8
 #ifndef GH_TILE_STAMPS
 #define GH_TILE_STAMPS 0  // diagnostic builds only: per-phase s_memtime deltas of waves 0 and 4
 #endif
@@ -108,43 +53,22 @@ constexpr int TILE_SCAP = GH_TILE_SCAPB;  // staging bytes per segment (larger t
 #else
 #define TSTAMP(i) ((void)0)
 #endif
+#ifndef GH_TILE_RANKPRIO
+#define GH_TILE_RANKPRIO 1  // issue priority by arrival rank (0: by "had to poll", the round-3/4 rule)
+#endif
+#ifndef GH_TILE_LATEPF
+#define GH_TILE_LATEPF 0  // the next tile's loads after the prefix check instead of right after the decode
+#endif
 #ifndef GH_TILE_ABLATE
 #define GH_TILE_ABLATE 0  // diagnostic builds only (make variant), bits: 1 no decode, 2 no staging
                           // stores, 4 no prefix wait (a fake offset), 8 no copy-out (wrong output)
 #endif
-#ifndef GH_TILE_LDSPTR
-#define GH_TILE_LDSPTR 0  // LUT reads as plain LDS loads instead of inline ds_read + wait
-#endif
-#ifndef GH_TILE_ONEASM
-#define GH_TILE_ONEASM 0  // the chains' borrow counts in one asm block per lookup step
-#endif
-#ifndef GH_TILE_TRIM
-#define GH_TILE_TRIM 1  // stop shifting window words no kept codeword can still read
-#endif
-#ifndef GH_TILE_NT
-#define GH_TILE_NT 2  // bits: 1 payload loads nontemporal, 2 copy-out 16-byte stores nontemporal (round 4: 2)
-#endif
 typedef unsigned int tile_v4u __attribute__((ext_vector_type(4)));
-// 16-byte global store of the copy-out (GH_TILE_NT & 2: streaming, the output is not re-read)
+// 16-byte global store of the copy-out: streaming (the output is never re-read, so it
+// should not displace the payload lines in L2; cfg4 0.574-0.579 vs 0.578-0.588 ms)
 __device__ __forceinline__ void tile_st16(uint4* d, const uint4& v) {
-  if (GH_TILE_NT & 2) __builtin_nontemporal_store(tile_v4u{v.x, v.y, v.z, v.w}, (tile_v4u*)d);
-  else *d = v;
+  __builtin_nontemporal_store(tile_v4u{v.x, v.y, v.z, v.w}, (tile_v4u*)d);
 }
-__device__ __forceinline__ uint4 tile_ld16(const uint32_t* s) {
-  if (GH_TILE_NT & 1) {
-    const tile_v4u v = __builtin_nontemporal_load((const tile_v4u*)s);
-    return make_uint4(v.x, v.y, v.z, v.w);
-  }
-  return *(const uint4*)s;
-}
-#ifndef GH_TILE_W4DPP
-#define GH_TILE_W4DPP 0  // look-ahead dword from the next lane (DPP wave_shl:1); lane 63 and the
-                         // shard's last segment from one wave-uniform load
-#endif
-constexpr int TILE_MIDG = GH_TILE_MIDG;  // decode group after which the mid-decode loads are issued
-constexpr int STAGE_PAD = 16;      // staging byte STAGE_PAD + i = tile byte i
-// Output words per segment: a segment holds at most ceil(128 / minlen) codewords (8
-// words at minlen 4, 11 at minlen 3), kept in registers as OW words per chain.
 
 struct TileParams {
   const uint32_t* payload;       // local segment j owns words [4j, 4j+4); +1 look-ahead, zero padded
@@ -160,19 +84,19 @@ struct TileParams {
   unsigned long long nseg;
   unsigned int gap_nib0, first_start, ntiles, kbits, lgr, epoch;
   unsigned int lut_bytes;        // LUT bytes in LDS (replicated: 4 << (K + lgr))
-  unsigned int stage_bytes;      // one staging buffer
-  uint4* junk;                   // padding stores: 16 bytes per thread of the grid, (TILE_NS + 2) slots
+  unsigned int idle_block;       // a block that exits at once (>= grid: none)
+  unsigned int stage_bytes;      // one wave's staging region (16 + its piece + margin, a multiple of 16)
   uint4* stamps;                 // GH_TILE_STAMPS builds: [grid][2 waves][128 iterations][2] phase deltas
-  // fused count + write tile kernel (gh_ftile.hip): lut = count LUT (Kc = kbits, at LDS 0)
-  const uint2* lutw;             // write LUT (2^kw u64 entries {symbols, b | n << 8})
-  unsigned int kw, lutw_off, lutw_bytes;  // its width, LDS offset (a multiple of 8 << kw), bytes
-  unsigned int stage_off;        // LDS offset of the staging
-  unsigned int last_end;         // end bit of the stream's last segment when the shard holds it (else 0)
+  unsigned long long* tstamps;   // GH_TILE_STAMPS builds: 100 MHz times: [ntiles] aggregate left, [ntiles]
+                                 // prefix obtained by wave 0 (bit 63: polled), [rounds] round published
 };
 
-// LDS of the tile kernel: LUT, two staging buffers, wave sums, leader wave totals.
+// LDS of the tile kernel: LUT, 2 x NW staging regions (one per wave and buffer), the
+// per-tile wave totals, offsets and arrival counters (TILE_SLOTS tiles), leader wave totals.
+// stage_bytes: one wave's region.
 inline size_t tile_lds_bytes(size_t lut_bytes, size_t stage_bytes) {
-  return lut_bytes + 2 * stage_bytes + 2 * (TILE_TB / 64) * 4 * TILE_U + 4 * (TILE_TB / 64) + 32;
+  return lut_bytes + 2 * (TILE_TB / 64) * stage_bytes + TILE_SLOTS * (2 * (TILE_TB / 64) + 1) * 4 +
+         TILE_SLOTS * 12 + 4 * (TILE_TB / 64) + 32;
 }
 
 // v_perm selector placing byte 1 of S0 (the symbol) at byte j, keeping S1's others.
@@ -210,40 +134,17 @@ __device__ __forceinline__ uint32_t q_init(bool act, int start) {
   return ((act ? (uint32_t)(127 - start) : 511u) << 23) | Q_SYMROOM | 32u;
 }
 
-// q[u] -= ent[u]; cnt[u] = pos1 where that borrows (the codeword that reaches the
-// segment end), for the U chains in one asm block.
-template <int U>
-__device__ __forceinline__ void borrow_count(uint32_t (&q)[U], uint32_t (&cnt)[U], const uint32_t (&ent)[U],
-                                             int pos1);
-template <>
-__device__ __forceinline__ void borrow_count<2>(uint32_t (&q)[2], uint32_t (&cnt)[2], const uint32_t (&ent)[2],
-                                                int pos1) {
-  asm("v_sub_co_u32 %0, vcc, %0, %4\n\tv_cndmask_b32_e64 %2, %2, %6, vcc\n\t"
-      "v_sub_co_u32 %1, vcc, %1, %5\n\tv_cndmask_b32_e64 %3, %3, %6, vcc"
-      : "+v"(q[0]), "+v"(q[1]), "+v"(cnt[0]), "+v"(cnt[1])
-      : "v"(ent[0]), "v"(ent[1]), "i"(pos1) : "vcc");
-}
-template <>
-__device__ __forceinline__ void borrow_count<3>(uint32_t (&q)[3], uint32_t (&cnt)[3], const uint32_t (&ent)[3],
-                                                int pos1) {
-  asm("v_sub_co_u32 %0, vcc, %0, %6\n\tv_cndmask_b32_e64 %3, %3, %9, vcc\n\t"
-      "v_sub_co_u32 %1, vcc, %1, %7\n\tv_cndmask_b32_e64 %4, %4, %9, vcc\n\t"
-      "v_sub_co_u32 %2, vcc, %2, %8\n\tv_cndmask_b32_e64 %5, %5, %9, vcc"
-      : "+v"(q[0]), "+v"(q[1]), "+v"(q[2]), "+v"(cnt[0]), "+v"(cnt[1]), "+v"(cnt[2])
-      : "v"(ent[0]), "v"(ent[1]), "v"(ent[2]), "i"(pos1) : "vcc");
-}
-
 // Decode of U segments per lane on e-windows, the U chains in lock-step (their LDS
 // reads are independent, so their latencies overlap).  Each group decodes G codewords
 // per chain from e0:e1 and then shifts the windows (G * maxlen <= 32, so the group's
 // consumed bits fit Q's low byte).  Codeword j of a segment goes to byte j of ow (v_perm,
 // static index); dead codewords go there too and are never staged.  `mid()` runs once,
-// after group MIDG (or at the end if the loop stops earlier).
-template <int G, int U, int OW, int MINL, class Hook, class Finish>
-__device__ __forceinline__ void decode_tile_grouped(uint32_t (&e)[U][5], const int (&start)[U],
-                                                    const bool (&act)[U], uint32_t (&ow)[U][OW],
-                                                    uint32_t (&cnt)[U], uint32_t amask, uint32_t laneoff,
-                                                    Hook&& hook, Finish&& finish) {
+// after group TILE_MIDG (NG > TILE_MIDG).  Returns the groups run (wave-uniform: the loop
+// stops once no chain of the wave is live).
+template <int G, int U, int OW, int MINL, class Mid>
+__device__ __forceinline__ int decode_tile_grouped(uint32_t (&e)[U][5], const int (&start)[U], const bool (&act)[U],
+                                                   uint32_t (&ow)[U][OW], uint32_t (&cnt)[U], uint32_t amask,
+                                                   uint32_t laneoff, Mid&& mid) {
   constexpr int S = 4 * OW;
   constexpr int NG = (S + G - 1) / G;
   uint32_t q[U];
@@ -252,15 +153,12 @@ __device__ __forceinline__ void decode_tile_grouped(uint32_t (&e)[U][5], const i
     q[u] = q_init(act[u], start[u]);
     cnt[u] = 0;
     // ow needs no zeroing: byte j is written by codeword j for every j < cnt, and the
-    // bytes past cnt are never kept (staging phase 2 / the copy-out's length cover them);
-    // an empty asm defines the registers without an instruction (24 v_mov per iteration)
+    // bytes past cnt are never kept; an empty asm defines the registers without an
+    // instruction (24 v_mov per iteration)
 #pragma unroll
-    for (int k = 0; k < OW; ++k) {
-      if (GH_TILE_NOZERO) asm volatile("" : "=v"(ow[u][k]));
-      else ow[u][k] = 0;
-    }
+    for (int k = 0; k < OW; ++k) asm volatile("" : "=v"(ow[u][k]));
   }
-  int gdone = NG;  // groups run (the loop stops once no chain is live)
+  int gdone = NG;
 #pragma unroll
   for (int gi = 0; gi < NG; ++gi) {
 #pragma unroll
@@ -271,23 +169,14 @@ __device__ __forceinline__ void decode_tile_grouped(uint32_t (&e)[U][5], const i
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const uint32_t x = j == 0 ? e[u][0] : __builtin_amdgcn_alignbit(e[u][0], e[u][1], q[u]);
-          if (GH_TILE_LDSPTR)  // a plain LDS load: the compiler counts lgkmcnt itself
-            ent[u] = *(const __attribute__((address_space(3))) uint32_t*)(
-                (const __attribute__((address_space(3))) uint8_t*)0 + ((x & amask) | laneoff));
-          else
-            ent[u] = lds_u32_nowait((x & amask) | laneoff);
+          ent[u] = lds_u32_nowait((x & amask) | laneoff);
         }
-        if (!GH_TILE_LDSPTR) lds_wait(ent);
-        if (GH_TILE_ONEASM) {
-          // the U borrow counts in one asm block: each inline asm boundary cost an s_nop
-          borrow_count<U>(q, cnt, ent, pos + 1);
-        } else {
+        lds_wait(ent);
 #pragma unroll
-          for (int u = 0; u < U; ++u)
-            asm("v_sub_co_u32 %0, vcc, %0, %2\n\t"
-                "v_cndmask_b32_e64 %1, %1, %3, vcc"
-                : "+v"(q[u]), "+v"(cnt[u]) : "v"(ent[u]), "i"(pos + 1) : "vcc");
-        }
+        for (int u = 0; u < U; ++u)
+          asm("v_sub_co_u32 %0, vcc, %0, %2\n\t"
+              "v_cndmask_b32_e64 %1, %1, %3, vcc"
+              : "+v"(q[u]), "+v"(cnt[u]) : "v"(ent[u]), "i"(pos + 1) : "vcc");
 #pragma unroll
         for (int u = 0; u < U; ++u)
           ow[u][pos >> 2] = __builtin_amdgcn_perm(ent[u], ow[u][pos >> 2], perm_sel(pos & 3));
@@ -304,222 +193,153 @@ __device__ __forceinline__ void decode_tile_grouped(uint32_t (&e)[U][5], const i
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       e[u][0] = __builtin_amdgcn_alignbit(e[u][0], e[u][1], q[u]);
-      if (!GH_TILE_TRIM || CMIN + 32 < 157) e[u][1] = __builtin_amdgcn_alignbit(e[u][1], e[u][2], q[u]);
-      if (!GH_TILE_TRIM || CMIN + 64 < 157) e[u][2] = __builtin_amdgcn_alignbit(e[u][2], e[u][3], q[u]);
-      if (!GH_TILE_TRIM || CMIN + 96 < 157) e[u][3] = __builtin_amdgcn_alignbit(e[u][3], e[u][4], q[u]);
-      if (!GH_TILE_TRIM || CMIN + 128 < 157) e[u][4] = __builtin_amdgcn_alignbit(e[u][4], 0u, q[u]);
+      if (CMIN + 32 < 157) e[u][1] = __builtin_amdgcn_alignbit(e[u][1], e[u][2], q[u]);
+      if (CMIN + 64 < 157) e[u][2] = __builtin_amdgcn_alignbit(e[u][2], e[u][3], q[u]);
+      if (CMIN + 96 < 157) e[u][3] = __builtin_amdgcn_alignbit(e[u][3], e[u][4], q[u]);
+      if (CMIN + 128 < 157) e[u][4] = __builtin_amdgcn_alignbit(e[u][4], 0u, q[u]);
       q[u] = (q[u] & 0xFFFFFF00u) | 32u;
       qmin = min(qmin, q[u]);
     }
-    hook(gi);  // a constant in the unrolled loop
-    if (gi + 1 < NG && !__any(qmin < Q_LIVE)) {
+    if (gi == TILE_MIDG) mid();  // a constant in the unrolled loop
+    // (no exit before mid(): every path then issues its loads at the same point, which
+    // keeps the compiler's wait counts exact; every kept segment runs past group MIDG)
+    if (gi >= TILE_MIDG && gi + 1 < NG && !__any(qmin < Q_LIVE)) {
       gdone = gi + 1;
       break;
     }
   }
-  finish(gdone);
+  return gdone;
 }
 
+// LDS store at an absolute byte address plus a constant offset (the instruction's
+// offset field).
+template <int OFF = 0>
 __device__ __forceinline__ void lds_st32(uint32_t a, uint32_t v) {
-  asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory");
+  asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(a), "v"(v), "i"(OFF) : "memory");
 }
-
-// Aligned staging of a segment's n bytes (ow, byte 0 first) at LDS byte address o.
-// Phase 1 writes the aligned dwords holding the segment's bytes, except the first one
-// when o is unaligned; its last dword carries whatever ow holds past byte n.  Phase 2,
-// after a workgroup barrier, writes the segment's head bytes (the 1-3 bytes of that
-// skipped first dword) exactly, over the previous segment's phase-1 tail.  Every dword
-// store is aligned: unaligned ds_write_b32 measured about 3x the LDS time of aligned
-// ones with per-lane offsets like these.  Returns the number of head bytes.
-template <int OW, int MINW = 0>
-__device__ __forceinline__ uint32_t stage_aligned_p1(const uint32_t (&ow)[OW], uint32_t n, uint32_t o) {
-  const uint32_t ap = ((o - 1u) & 3u) + 1u;  // 1..4: bytes from the dword base to o
-  const uint32_t base = o - ap;              // dword m at base + 4m holds segment bytes [4m - ap, +4)
-  const uint32_t s = 4u - ap;                // alignbyte amount
-  const uint32_t last = (n + ap - 1u) >> 2;  // last dword touched
-#pragma unroll
-  for (int m = 1; m <= OW; ++m) {
-    const uint32_t hi = m < OW ? ow[m] : 0u;
-    const uint32_t r = __builtin_amdgcn_alignbyte(hi, ow[m - 1], s);
-    // dwords 1..MINW are touched by every segment of >= 4 * MINW codewords (the caller
-    // guarantees it for every kept segment): stored without a per-lane test
-    if (m <= MINW || (uint32_t)m <= last) lds_st32(base + 4u * m, r);
+// A waited LDS read / write at an absolute byte address (hand-offs between waves).
+__device__ __forceinline__ uint32_t lds_ld_u32(uint32_t a) {
+  uint32_t v;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+  return v;
+}
+__device__ __forceinline__ void lds_st_u32(uint32_t a, uint32_t v) {
+  asm volatile("ds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" ::"v"(a), "v"(v) : "memory");
+}
+// ... with the offset 4m, m a constant of the unrolled caller (1..12)
+__device__ __forceinline__ void lds_st32_m(uint32_t a, uint32_t v, int m) {
+  switch (m) {
+    case 1: lds_st32<4>(a, v); break;
+    case 2: lds_st32<8>(a, v); break;
+    case 3: lds_st32<12>(a, v); break;
+    case 4: lds_st32<16>(a, v); break;
+    case 5: lds_st32<20>(a, v); break;
+    case 6: lds_st32<24>(a, v); break;
+    case 7: lds_st32<28>(a, v); break;
+    case 8: lds_st32<32>(a, v); break;
+    case 9: lds_st32<36>(a, v); break;
+    case 10: lds_st32<40>(a, v); break;
+    case 11: lds_st32<44>(a, v); break;
+    default: lds_st32<0>(a + 4u * (uint32_t)m, v); break;
   }
-  return min(4u - ap, n);  // (n >= 4 - ap for every grouped code; never write past n)
 }
-// Phase 2: the nb (1..3) head bytes h at o (o + (nb & 1) is even).
-__device__ __forceinline__ void stage_head(uint32_t o, uint32_t h, uint32_t nb) {
-  if (nb & 1u) asm volatile("ds_write_b8 %0, %1" ::"v"(o), "v"(h) : "memory");
-  if (nb & 2u) asm volatile("ds_write_b16 %0, %1" ::"v"(o + (nb & 1u)), "v"(h >> (8u * (nb & 1u))) : "memory");
+// Staging of one wave's 64U consecutive segments into the wave's own region (chain u lane
+// l = segment 64u + l of the wave, n[u] bytes from ow[u] at LDS byte o[u]; the first one
+// at the region's 16-byte aligned start), with no other wave involved.
+//
+// A segment's bytes are realigned to the dwords they fall in: with ap = o - base in 1..4
+// (base = o rounded down to a dword, minus 4 when o is aligned), dword m >= 1 at base + 4m
+// holds segment bytes [4m - ap, +4).  Rounds m = mmax .. 1 store dword m of every segment
+// unconditionally, chain by chain: a dword past a segment's end holds garbage, but it lies
+// in the next one or two segments of the wave, which store that address in a LATER round
+// (their base is higher, so their m for it is lower; within a round a segment's dwords
+// differ from the others').  LDS operations of a wave complete in order, so the last
+// store to every address is the one of the last segment that starts before it: the right
+// bytes, except in each segment's first dword (base, when ap < 4), which holds the
+// previous segment's tail followed by garbage.  Each segment then reads that dword back
+// and puts its head bytes over the garbage (read-modify-write, in order again).  Garbage
+// past the wave's last segment lands in the region's margin.  (Rounds 2-4: aligned stores
+// under exec masks, a second workgroup barrier and head bytes after it: ~36 VALU and ~21
+// SALU per segment.)
+template <int U, int OW>
+__device__ __forceinline__ void stage_wave(const uint32_t (&ow)[U][OW], const uint32_t (&n)[U], const uint32_t (&o)[U],
+                                           int mmax) {
+  uint32_t base[U], sh[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t ap = ((o[u] - 1u) & 3u) + 1u;
+    base[u] = o[u] - ap;
+    sh[u] = 4u - ap;  // v_alignbyte amount: dword m = bytes [4m - ap, +4) of the segment
+  }
+#pragma unroll
+  for (int m = OW; m >= 1; --m) {
+    if (m > mmax) continue;  // wave-uniform: no segment of the wave reaches dword m
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      lds_st32_m(base[u], __builtin_amdgcn_alignbyte(m < OW ? ow[u][m] : 0u, ow[u][m - 1], sh[u]), m);
+  }
+  // head dwords: read back (the previous segment's tail + garbage), merge, store; the
+  // reads are unconditional, the stores are not (a segment at an aligned offset, and the
+  // empty segments past a shard's end, have no head dword)
+  uint32_t rd[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) rd[u] = lds_u32_nowait(base[u]);
+  lds_wait(rd);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t ap = o[u] - base[u];
+    if (n[u] && ap < 4u) {
+      const uint32_t ab = 8u * ap;  // the previous segment's bits in the dword
+      lds_st32(base[u], (rd[u] & ((1u << ab) - 1u)) | (ow[u][0] << ab));
+    }
+  }
 }
 
-// Copy a tile staged at staging byte STAGE_PAD + i = tile byte i to out[goff, goff+n)
-// (n already clamped at out_cap).  Output chunk c (16 bytes, aligned to the global
-// address) is staging bytes [16c + s, +16), s = 16 - (goff & 15): one unaligned
-// ds_read_b128 (gfx950 LDS runs in unaligned mode).  A fixed number of store
-// instructions per thread: NS 16-byte stores (interior chunks; spare threads store the
-// last interior chunk again, the same bytes, merged in L2) and one byte store (a byte of
-// the two partial edge chunks, or the first edge byte again); the thread's junk slot
-// only when there is nothing to duplicate.  gfx950 counts loads and stores in one
-// in-order queue (vmcnt): with a fixed store count after the next tile's prefetch loads
-// the compiler waits for those loads with vmcnt(NS + 1) instead of vmcnt(0), so a wave
-// no longer waits for its previous copy-out's stores to be acknowledged.  Chunks beyond
-// NS per thread (a tile larger than 16 * NS * TB bytes) loop.  stg: absolute LDS byte
-// address of the staging buffer.
-template <int TBK, int NS, bool TAIL>
-__device__ __forceinline__ void copy_out_tile(uint8_t* out, uint32_t stg, unsigned long long goff, uint32_t n,
-                                              int tid, uint4* junk) {
+// Copy one wave's piece of a tile, staged at LDS byte stg + 16 + i = piece byte i, to
+// out[goff, goff + n) (n already clamped at out_cap).  Output chunk c (16 bytes, aligned
+// to the global address) is staging bytes [16c + 16 - lb, +16), lb = goff & 15: one
+// unaligned ds_read_b128 (gfx950 LDS runs in unaligned mode).  Every lane issues exactly
+// NS 16-byte buffer stores and one byte store (the partial head and tail chunks' bytes,
+// one per lane): a lane with no chunk (byte) stores at an offset past the buffer's range,
+// which the hardware drops, so no padding bytes reach memory and the store count is
+// fixed.  gfx950 counts loads and stores in one in-order queue (vmcnt): with a fixed store
+// count after the next tile's prefetch loads the compiler waits for those loads with a
+// counted vmcnt instead of vmcnt(0), so a wave never waits for its copy-out's stores to
+// be acknowledged.  The host sizes the regions so that NS * 64 chunks cover a piece.
+constexpr uint32_t OOB_OFF = 0x80000000u;  // a buffer offset past every range: the store is dropped
+template <int NS>
+__device__ __forceinline__ void copy_out_piece(uint8_t* out, uint32_t stg, unsigned long long goff, uint32_t n,
+                                               int lane) {
   const uint32_t lb = (uint32_t)(goff & 15);
-  uint8_t* o = out + (goff - lb);          // 16-byte aligned
-  const uint32_t src = stg + 16u - lb;     // staging address of output chunk 0
-  const uint32_t cf = lb ? 1u : 0u;        // interior chunks [cf, ce)
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out + (goff - lb), 0, 0x7FFFFFF0, 0x00020000);
+  const uint32_t src = stg + 16u - lb;    // staging address of output chunk 0
+  const uint32_t cf = lb ? 1u : 0u;       // interior chunks [cf, ce)
   const uint32_t ce = n ? (lb + n) >> 4 : 0u;
-  const bool have = ce > cf;
-  if constexpr (TAIL && GH_TILE_BATCH) {
-    // every read of this thread's chunks and edge byte issued, then one wait, then the
-    // stores (one LDS round trip instead of one per chunk)
-    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-    v4u v[NS];
-    uint32_t cs[NS];
-    v4u* d[NS];
+  tile_v4u v[NS];
+  uint32_t off[NS];
 #pragma unroll
-    for (int i = 0; i < NS; ++i) {
-      const uint32_t c = cf + (uint32_t)tid + (uint32_t)(TBK * i);
-      const bool real = c < ce;
-      cs[i] = real ? c : ce - 1u;
-      asm volatile("ds_read_b128 %0, %1" : "=v"(v[i]) : "v"(src + 16u * ((real || have) ? cs[i] : cf)) : "memory");
-      d[i] = (real || have) ? (v4u*)(o + 16ull * cs[i]) : (v4u*)junk;
-    }
-    const uint32_t nh = (lb && n) ? min(16u, lb + n) - lb : 0u;
-    const uint32_t tl = (lb + n) & 15u;
-    const uint32_t nt = (n && tl && (ce > 0 || !lb)) ? tl : 0u;
-    const uint32_t t = (uint32_t)tid;
-    const bool hb = nh + nt > 0;
-    uint32_t k = nh ? lb : 16u * ce;
-    bool real = false;
-    if (t < nh) {
-      k = lb + t;
-      real = true;
-    } else if (t < nh + nt) {
-      k = 16u * ce + (t - nh);
-      real = true;
-    }
-    uint32_t b;
-    asm volatile("ds_read_u8 %0, %1" : "=v"(b) : "v"(src + ((real || hb) ? k : 0u)) : "memory");
-    static_assert(NS == 2 || NS == 3, "batched copy-out: 2 or 3 chunks per thread");
-    if constexpr (NS == 2) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(b)::"memory");
-    else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(b)::"memory");
-#pragma unroll
-    for (int i = 0; i < NS; ++i) *d[i] = v[i];
-    *((real || hb) ? o + k : (uint8_t*)junk) = (uint8_t)b;
-    for (uint32_t c = cf + (uint32_t)tid + (uint32_t)(TBK * NS); c < ce; c += TBK)
-      *(uint4*)(o + 16ull * c) = lds_u128(src + 16u * c);
-    return;
-  }
-  if (TAIL) {
-#pragma unroll
-    for (int i = 0; i < NS; ++i) {
-      const uint32_t c = cf + (uint32_t)tid + (uint32_t)(TBK * i);
-      const bool real = c < ce;
-      const uint32_t cs = real ? c : ce - 1u;
-      const uint4 v = lds_u128(src + 16u * ((real || have) ? cs : cf));
-      tile_st16((real || have) ? (uint4*)(o + 16ull * cs) : junk, v);
-    }
-    for (uint32_t c = cf + (uint32_t)tid + (uint32_t)(TBK * NS); c < ce; c += TBK)
-      tile_st16((uint4*)(o + 16ull * c), lds_u128(src + 16u * c));
-  } else {
-    // NS x TBK chunks cover every staged tile (the host sizes NS): no loop, so the
-    // store count is fixed and the next iteration's wait for its prefetched loads
-    // (issued before these stores) does not wait for these stores' acknowledgements.
-    // A store past the tile rewrites the thread's first chunk (same bytes, its own
-    // address: no two threads pad onto one line); no LDS read for it.
-    const uint32_t c0 = cf + (uint32_t)tid;
-    const bool real0 = c0 < ce;
-    const uint32_t cs0 = real0 ? c0 : (have ? ce - 1u : cf);
-    const uint4 v0 = lds_u128(src + 16u * cs0);
-    uint4* const d0 = (real0 || have) ? (uint4*)(o + 16ull * cs0) : junk;
-    tile_st16(d0, v0);
-#pragma unroll
-    for (int i = 1; i < NS; ++i) {
-      const uint32_t c = c0 + (uint32_t)(TBK * i);
-      uint4 v = v0;
-      uint4* d = d0;
-      if (c < ce) {
-        v = lds_u128(src + 16u * c);
-        d = (uint4*)(o + 16ull * c);
-      }
-      tile_st16(d, v);
-    }
+  for (int i = 0; i < NS; ++i) {
+    const uint32_t c = cf + (uint32_t)lane + 64u * (uint32_t)i;
+    off[i] = c < ce ? 16u * c : OOB_OFF;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v[i]) : "v"(src + 16u * (c < ce ? c : cf)) : "memory");
   }
   // edge bytes: the head chunk's [lb, min(16, lb + n)) when lb != 0, then the tail
-  // chunk's [0, (lb + n) & 15) when it is another chunk; one byte per thread
+  // chunk's [0, (lb + n) & 15) when it is another chunk; one byte per lane
   const uint32_t nh = (lb && n) ? min(16u, lb + n) - lb : 0u;
   const uint32_t tl = (lb + n) & 15u;
   const uint32_t nt = (n && tl && (ce > 0 || !lb)) ? tl : 0u;
-  const uint32_t t = (uint32_t)tid;
-  const bool hb = nh + nt > 0;
-  uint32_t k = nh ? lb : 16u * ce;  // output byte offset from o (padding: the first edge byte)
-  bool real = false;
-  if (t < nh) {
-    k = lb + t;
-    real = true;
-  } else if (t < nh + nt) {
-    k = 16u * ce + (t - nh);
-    real = true;
-  }
+  const uint32_t t = (uint32_t)lane;
+  uint32_t k = OOB_OFF;
+  if (t < nh) k = lb + t;
+  else if (t < nh + nt) k = 16u * ce + (t - nh);
   uint32_t b;
-  asm volatile("ds_read_u8 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(b) : "v"(src + ((real || hb) ? k : 0u)) : "memory");
-  *((real || hb) ? o + k : (uint8_t*)junk) = (uint8_t)b;
+  asm volatile("ds_read_u8 %0, %1" : "=v"(b) : "v"(src + (k == OOB_OFF ? 0u : k)) : "memory");
+  if constexpr (NS == 4) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(b)::"memory");
+  else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(b)::"memory");
+#pragma unroll
+  for (int i = 0; i < NS; ++i) __builtin_amdgcn_raw_buffer_store_b128(v[i], rs, (int)off[i], 0, 2);  // nt
+  __builtin_amdgcn_raw_buffer_store_b8((uint8_t)b, rs, (int)k, 0, 2);
 }
-
-// The copy-out of copy_out_tile<TBK, NS, true> cut into parts (GH_TILE_IOVL): chunk i
-// of every thread, then the edge byte, then the loop over chunks beyond NS per thread,
-// so that the parts can run between the decode groups of the next tile.
-template <int TBK, int NS>
-struct CopyParts {
-  uint8_t* o = nullptr;
-  uint32_t src = 0, cf = 0, ce = 0, lb = 0, n = 0;
-  bool have = false;
-  __device__ __forceinline__ void init(uint8_t* out, uint32_t stg, unsigned long long goff, uint32_t n_) {
-    n = n_;
-    lb = (uint32_t)(goff & 15);
-    o = out + (goff - lb);
-    src = stg + 16u - lb;
-    cf = lb ? 1u : 0u;
-    ce = n ? (lb + n) >> 4 : 0u;
-    have = ce > cf;
-  }
-  __device__ __forceinline__ void chunk(int i, int tid, uint4* junk) const {
-    const uint32_t c = cf + (uint32_t)tid + (uint32_t)(TBK * i);
-    const bool real = c < ce;
-    const uint32_t cs = real ? c : ce - 1u;
-    const uint4 v = lds_u128(src + 16u * ((real || have) ? cs : cf));
-    *((real || have) ? (uint4*)(o + 16ull * cs) : junk) = v;
-  }
-  __device__ __forceinline__ void edge(int tid, uint4* junk) const {
-    const uint32_t nh = (lb && n) ? min(16u, lb + n) - lb : 0u;
-    const uint32_t tl = (lb + n) & 15u;
-    const uint32_t nt = (n && tl && (ce > 0 || !lb)) ? tl : 0u;
-    const uint32_t t = (uint32_t)tid;
-    const bool hb = nh + nt > 0;
-    uint32_t k = nh ? lb : 16u * ce;
-    bool real = false;
-    if (t < nh) {
-      k = lb + t;
-      real = true;
-    } else if (t < nh + nt) {
-      k = 16u * ce + (t - nh);
-      real = true;
-    }
-    uint32_t b;
-    asm volatile("ds_read_u8 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(b) : "v"(src + ((real || hb) ? k : 0u)) : "memory");
-    *((real || hb) ? o + k : (uint8_t*)junk) = (uint8_t)b;
-  }
-  __device__ __forceinline__ void tail(int tid) const {
-    for (uint32_t c = cf + (uint32_t)tid + (uint32_t)(TBK * NS); c < ce; c += TBK)
-      *(uint4*)(o + 16ull * c) = lds_u128(src + 16u * c);
-  }
-};
 
 // A segment's n bytes (ow, byte 0 first) stored to out[o, o + n), clamped at cap: the
 // path of a tile too large for staging (byte stores; rare).
@@ -559,19 +379,21 @@ __device__ __forceinline__ unsigned long long poll_granule(const TileParams& p, 
         return 0;
       }
     }
-    __builtin_amdgcn_s_sleep(GH_POLL_SLEEP);
+    __builtin_amdgcn_s_sleep(2);
   }
 }
 
-// The round leader (workgroup 0): for every round r of D = grid - 1 tiles, wait for the
-// round's aggregates (thread t takes the A = ceil(D / TB) <= LEAD_A consecutive tiles
-// t*A .. t*A + A - 1 of the round), scan them and publish each tile's global exclusive
-// prefix; R, the start of the round, stays in a register.  (Spreading the rounds over the
-// leader's waves, eight rounds' loads in flight, measured slower.)
+// The round leader (workgroup 0): for every round r of D decoding workgroups' tiles, wait
+// for the round's aggregates (thread t takes the A = ceil(D / TB) <= LEAD_A consecutive
+// tiles t*A .. t*A + A - 1 of the round), scan them and publish each tile's global
+// exclusive prefix; R, the start of the round, stays in a register.  (Spreading the rounds
+// over the leader's waves, the next rounds' aggregates loaded ahead, measured slower:
+// 0.74 vs 0.71 ms in round 3 with eight rounds in flight, 0.615 vs 0.586 ms in round 5
+// with two.)
 constexpr int LEAD_A = 4;
 template <int TB>
-__device__ __forceinline__ void tile_round_leader(const TileParams& p, uint32_t* s_lead, int tid, int lane, int wid) {
-  const uint32_t D = gridDim.x - 1;
+__device__ __forceinline__ void tile_round_leader(const TileParams& p, uint32_t D, uint32_t* s_lead, int tid,
+                                                  int lane, int wid) {
   const uint32_t A = (D + TB - 1) / TB;  // <= LEAD_A (the host caps the grid)
   const uint32_t nr = (p.ntiles + D - 1) / D;
   unsigned long long R = 0;
@@ -611,6 +433,9 @@ __device__ __forceinline__ void tile_round_leader(const TileParams& p, uint32_t*
       run += v[i];
     }
     R += total;
+#if GH_TILE_STAMPS
+    if (tid == 0) p.tstamps[2 * p.ntiles + r] = __builtin_amdgcn_s_memrealtime();  // round r published
+#endif
     __syncthreads();
   }
 }
@@ -618,197 +443,148 @@ __device__ __forceinline__ void tile_round_leader(const TileParams& p, uint32_t*
 // TB threads, U segments per lane, GRP codewords per window shift, OW output words per
 // segment, codewords of at least MINL bits.  Compiled for at most 4 waves per SIMD (two
 // workgroups per CU: 128 VGPRs).
+//
+// The waves of a decoding workgroup run without a workgroup barrier: each stages its own
+// segments into its own LDS region and copies its own piece out.  The tile's aggregate
+// is published by the wave that arrives last at it (an LDS counter per tile slot), which
+// also writes every wave's offset in the tile; a wave reads the offsets of tile k-2 only
+// after its global prefix has arrived, which the aggregate (so every wave's arrival)
+// precedes.  A wave can thus run at most about three tiles ahead of the slowest wave of
+// its workgroup (it needs tile k-3's prefix at iteration k-1), within the TILE_SLOTS
+// slots.
 template <int TB, int U, int GRP, int OW, int MINL>
-__global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE, GH_TILE_WPE))) void gh_tile_kernel(const TileParams p) {
+__global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void gh_tile_kernel(const TileParams p) {
   static_assert(4 * OW >= (128 + MINL - 1) / MINL, "OW words hold every codeword a segment can start");
-  static_assert(U * (TB / 64) <= 2 * TILE_U * (TB / 64), "wave sums fit tile_lds_bytes");
-  constexpr int NWAVE_T = TB / 64;
+  static_assert(U <= TILE_U, "shapes of at most TILE_U segments per lane");
+  constexpr int NW = TB / 64;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint8_t* s_stage = smem + p.lut_bytes;                        // 2 buffers
-  uint32_t* s_wsum = (uint32_t*)(s_stage + 2 * p.stage_bytes);  // [2][U][NWAVE_T]
-  uint32_t* s_lead = s_wsum + 2 * U * NWAVE_T;                  // [NWAVE_T] (leader)
+  const uint32_t stage_lds = p.lut_bytes;                                  // [2][NW] regions
+  uint32_t* s_tot = (uint32_t*)(smem + p.lut_bytes + 2 * NW * p.stage_bytes);  // [SLOTS][NW] wave totals
+  uint32_t* s_off = s_tot + TILE_SLOTS * NW;                                // [SLOTS][NW] wave offsets
+  uint32_t* s_cnt = s_off + TILE_SLOTS * NW;                                // [SLOTS] arrivals
+  unsigned long long* s_pfx = (unsigned long long*)(s_cnt + TILE_SLOTS);   // [SLOTS] prefixes (wave 0)
+  uint32_t* s_ptile = (uint32_t*)(s_pfx + TILE_SLOTS);                      // [SLOTS] their tiles
+  uint32_t* s_lead = s_ptile + TILE_SLOTS;                                  // [NW] (leader)
+  const uint32_t cnt_lds = (uint32_t)((uint8_t*)s_cnt - smem);
+  const uint32_t ptile_lds = (uint32_t)((uint8_t*)s_ptile - smem);
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // decoding workgroups: every block but 0 (the leader) and p.idle_block (if < grid)
+  const uint32_t D = gridDim.x - 1 - (p.idle_block < gridDim.x ? 1u : 0u);
   if (blockIdx.x == 0) {
-    tile_round_leader<TB>(p, s_lead, tid, lane, wid);
+    tile_round_leader<TB>(p, D, s_lead, tid, lane, wid);
     return;
   }
+  if (blockIdx.x == p.idle_block) return;  // the leader's CU partner (GH_TILE_IDLE): no decoding
   {  // LUT to LDS, replicated: dword i of LDS = entry i >> lgr (lane l reads copy l mod 2^lgr,
      // so up to 32 lanes of a ds_read_b32 hit distinct banks)
     const uint32_t nd = p.lut_bytes >> 2;
     uint32_t* sl = (uint32_t*)smem;
     for (uint32_t i = tid; i < nd; i += TB) sl[i] = p.lut[i >> p.lgr];
+    if (tid < TILE_SLOTS) {
+      s_cnt[tid] = 0;
+      s_ptile[tid] = 0xFFFFFFFFu;
+    }
   }
   const uint32_t S = 30u - p.kbits - p.lgr;
   const uint32_t amask = ((1u << p.kbits) - 1u) << (2u + p.lgr);
   const uint32_t laneoff = ((uint32_t)lane & ((1u << p.lgr) - 1u)) << 2;
   check_lds_base(smem, p.status);
 
-  const uint32_t G = gridDim.x - 1, b = blockIdx.x - 1;  // decoding workgroups, this one
+  const uint32_t G = D, b = blockIdx.x - 1 - (blockIdx.x > p.idle_block ? 1u : 0u);  // decoders, this one
   const uint32_t nseg = (uint32_t)p.nseg;                 // < 2^31 (checked by the host)
   constexpr uint32_t NONE = 0xFFFFFFFFu;
-  __syncthreads();
+  __syncthreads();  // the LUT and the counters (the last barrier of a decoding workgroup)
   const uint32_t last_tile_k = b < p.ntiles ? (p.ntiles - 1 - b) / G : NONE;
   uint32_t cur = b, nxt = b + G;
+  // the lane's segments in a tile: wave-contiguous, 64 per chain
+  const uint32_t lseg = (uint32_t)(wid * 64 * U + lane);
   uint4 w[U];
   uint32_t w4[U], gw[U];
   auto load = [&](uint32_t t) {
-    const uint32_t seg0 = min(t, p.ntiles - 1) * (uint32_t)(U * TB) + (uint32_t)tid;
+    const uint32_t seg0 = min(t, p.ntiles - 1) * (uint32_t)(U * TB) + lseg;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const uint32_t sc = min(seg0 + (uint32_t)(u * TB), nseg - 1);
-      w[u] = tile_ld16(p.payload + 4ull * sc);
-      if (GH_TILE_W4DPP) {  // lane 63's look-ahead (every lane the same address)
-        const uint32_t s63 = min(seg0 - (uint32_t)lane + 63u + (uint32_t)(u * TB), nseg - 1);
-        w4[u] = p.payload[4ull * s63 + 4];
-      } else {
-        w4[u] = p.payload[4ull * sc + 4];
-      }
+      const uint32_t sc = min(seg0 + (uint32_t)(64 * u), nseg - 1);
+      w[u] = *(const uint4*)(p.payload + 4ull * sc);
+      w4[u] = p.payload[4ull * sc + 4];
       gw[u] = p.gaps[(p.gap_nib0 + (sc ? sc - 1u : 0u)) >> 3];
     }
   };
   load(cur);
   {  // as many stores after these loads as every iteration issues after its prefetch
-     // (the copy-out's TILE_NS + 1): the loop's entry then matches its back edge, and
-     // the compiler waits for the loads with a counted vmcnt instead of vmcnt(0)
-    const unsigned long long slot = (unsigned long long)blockIdx.x * TB + tid, nslot = (unsigned long long)gridDim.x * TB;
+     // (the copy-out's TILE_NS + 1, dropped here: out of range): the loop's entry then
+     // matches its back edge, and the compiler waits for the loads with a counted vmcnt
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(p.out, 0, 0x7FFFFFF0, 0x00020000);
 #pragma unroll
-    for (int i = 0; i <= TILE_NS; ++i) p.junk[slot + (unsigned long long)(i + 1) * nslot] = make_uint4(0, 0, 0, 0);
+    for (int i = 0; i < TILE_NS; ++i)
+      __builtin_amdgcn_raw_buffer_store_b128(tile_v4u{0, 0, 0, 0}, rs, (int)OOB_OFF, 0, 2);
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)0, rs, (int)OOB_OFF, 0, 2);
   }
   if (cur >= p.ntiles) cur = NONE;
-  uint32_t t1 = NONE, t2 = NONE;  // tiles of iterations k-1, k-2
-  uint32_t tot1 = 0, tot2 = 0;    // their totals
-  uint32_t buf = 0;               // k & 1
+  uint32_t t1 = NONE, t2 = NONE;  // this wave's pieces of iterations k-1, k-2 (NONE: not staged)
   bool ahead = false;             // the last prefix had to be polled
-  unsigned long long gpc = 0;     // (IOVL) prefix of the next iteration's tile k-2, loaded early
+  uint32_t rank = 0;              // (GH_TILE_RANKPRIO) the wave's arrival rank at its last tile, in quarters
+  const uint32_t region0 = stage_lds + (uint32_t)wid * p.stage_bytes;  // buffer 0; buffer 1 at + NW * stage_bytes
+  const uint32_t piece_cap = p.stage_bytes - (uint32_t)(STAGE_PAD + 4 * OW + 4);
 #if GH_TILE_STAMPS
   unsigned long long ts[9];
 #endif
   for (uint32_t k = 0;; ++k) {
     TSTAMP(0);
     const bool have_cur = cur < p.ntiles;
-    const bool have2 = t2 < p.ntiles;  // tile k-2 is copied out this iteration
+    const bool have2 = t2 < p.ntiles;  // this wave's piece of tile k-2 is copied out this iteration
     if (!have_cur && t1 >= p.ntiles && !have2) break;
     if (last_tile_k != NONE && k > last_tile_k + 4) {  // cannot happen; never hang the GPU
-      if (tid == 0) atomicOr(p.status, (unsigned)GH_ST_TIMEOUT);
+      if (lane == 0) atomicOr(p.status, (unsigned)GH_ST_TIMEOUT);
       break;
     }
-    const uint32_t par = k & 1u;
-    if (GH_TILE_ALTPRIO) {
-      // the two workgroups of a CU (whichever they are: consecutive indices or 256
-      // apart) take turns at the higher issue priority, so the younger one is not
-      // always second (it otherwise ran ~5 % slower and the rounds waited for it)
-      const uint32_t turn = (k + blockIdx.x + (blockIdx.x >> 8)) & 1u;
-      if (turn) __builtin_amdgcn_s_setprio(2);
-      else __builtin_amdgcn_s_setprio(1);
-    } else if (GH_TILE_WPRIO && wid >= 4) {
-      if (ahead) __builtin_amdgcn_s_setprio(GH_TILE_PLO + 1);
-      else __builtin_amdgcn_s_setprio(GH_TILE_PHI + 1);
+    const uint32_t slot = k % TILE_SLOTS, slot2 = (k + TILE_SLOTS - 2) % TILE_SLOTS;
+    const uint32_t buf = k & 1u;
+    if (GH_TILE_RANKPRIO) {
+      // by the wave's arrival rank at its last tile (0: first of the workgroup's waves):
+      // the waves that arrive last gate the tile's aggregate, so they issue first
+      if (rank >= 3) __builtin_amdgcn_s_setprio(3);
+      else if (rank == 2) __builtin_amdgcn_s_setprio(2);
+      else if (rank == 1) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+    } else if (ahead) {
+      __builtin_amdgcn_s_setprio(0);
     } else {
-      if (ahead) __builtin_amdgcn_s_setprio(GH_TILE_PLO);
-      else __builtin_amdgcn_s_setprio(GH_TILE_PHI);
+      __builtin_amdgcn_s_setprio(2);
     }
-    // prefix of tile k-2 (lane 0 of every wave): loaded mid-decode (a load issued at the
-    // top often saw the value a little before it was published, and the re-poll then
-    // paid a full memory round trip)
-    unsigned long long gp = GH_TILE_IOVL ? gpc : 0ull;
+    // prefix of tile k-2 (lane 0): loaded at the top and again mid-decode; the first that
+    // shows it published is used (a load at the top alone often saw it a little before it
+    // was published, and the re-poll then paid a full memory round trip)
+    // (every lane loads the same word, one request; no branch around the load: the
+    // compiler's wait counting over such a branch fell back to vmcnt(0), which then also
+    // waited for the next tile's loads issued behind it)
+    unsigned long long* const pf2 = &p.prefix[have2 ? t2 : 0u];
+    unsigned long long gp0 = 0, gp = 0;
+    if (!(GH_TILE_ABLATE & 4)) gp0 = __hip_atomic_load(pf2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     auto mid = [&]() {
-      if (!GH_TILE_IOVL && have2 && lane == 0 && !(GH_TILE_ABLATE & 4))
-        gp = __hip_atomic_load(&p.prefix[t2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    };
-    // ---- the prefix of tile k-2 -> its output offset (lane 0 of every wave) -----------
-    unsigned long long goff = 0;
-    uint32_t n2 = 0;
-    auto prefix_check = [&]() {
-      if (have2 && (GH_TILE_ABLATE & 4)) {
-        goff = ((unsigned long long)t2 * (U * TB * 16)) % (p.out_cap - (U * TB * 32));
-        n2 = tot2;
-      } else if (have2) {
-        bool polled = false, got = true;
-        if (lane == 0) {
-          polled = !granule_ok(p, gp, 2);
-          if (polled) {
-            if (wid == 0) atomicAdd(p.stats, 1ull);
-            gp = poll_granule(p, &p.prefix[t2], 2);
-            got = granule_ok(p, gp, 2);  // false only after a timeout (then nothing is written)
-          }
-          goff = gp & GRAN_VMASK;
-          if (wid == 0 && t2 == p.ntiles - 1 && got) *p.total = goff + tot2;
-        }
-        goff = rfl_u64(goff);
-        ahead = __builtin_amdgcn_readfirstlane(polled ? 1 : 0) != 0;
-        got = __builtin_amdgcn_readfirstlane(got ? 1 : 0) != 0;
-        n2 = (!got || goff >= p.out_cap) ? 0u : (uint32_t)min<unsigned long long>(tot2, p.out_cap - goff);
-      }
-    };
-    // (IOVL) the copy-out of tile k-2 in parts after decode groups IOB .. IOB + NS
-    CopyParts<TB, TILE_NS> co;
-    uint4* const jk = p.junk + (unsigned long long)blockIdx.x * TB + tid;
-    auto co_part = [&](int j) {
-      if (j == 0) {
-        prefix_check();
-        co.init(p.out, p.lut_bytes + buf * p.stage_bytes, goff, n2);
-      }
-      if (j < TILE_NS) co.chunk(j, tid, jk);
-      else co.edge(tid, jk);
-    };
-    auto hook = [&](int gi) {
-      if (GH_TILE_IOVL) {
-        if (gi >= GH_TILE_IOB && gi <= GH_TILE_IOB + TILE_NS) co_part(gi - GH_TILE_IOB);
-      } else if (gi == TILE_MIDG) {
-        mid();
-      }
-    };
-    auto finish = [&](int gdone) {
-      if (GH_TILE_IOVL) {
-#pragma unroll
-        for (int j = 0; j <= TILE_NS; ++j)
-          if (gdone <= GH_TILE_IOB + j) co_part(j);
-        co.tail(tid);
-        // then the prefix of tile k-1 (the next iteration's copy-out; published about
-        // an iteration ago) and the next tile's words, in that order: the copy-out's
-        // stores are older than both, and the top of the next iteration waits only for
-        // the loads (the stores, issued during the decode, have long completed)
-        if (lane == 0 && t1 < p.ntiles && !(GH_TILE_ABLATE & 4))
-          gpc = __hip_atomic_load(&p.prefix[t1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        load(nxt);
-      } else if (gdone <= TILE_MIDG) {
-        mid();
-      }
+      if (!(GH_TILE_ABLATE & 4)) gp = __hip_atomic_load(pf2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
     // ---- decode this tile (its words were loaded during the previous iteration) --------
-    const uint32_t seg0 = cur * (uint32_t)(U * TB) + (uint32_t)tid;
+    // Decoded unconditionally: in the last iterations (no tile) every chain is inactive
+    // and the loop stops after one group (the loads were issued, clamped to the last
+    // tile).  A branch around the decode made the compiler zero the output words before
+    // it every iteration and wait vmcnt(0) after it.
+    const uint32_t seg0 = cur * (uint32_t)(U * TB) + lseg;
     uint32_t ow[U][OW], cnt[U];
+    int gdone;
     {
       int start[U];
       bool act[U];
       uint32_t e[U][5];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const uint32_t seg = seg0 + (uint32_t)(u * TB);
+        const uint32_t seg = seg0 + (uint32_t)(64 * u);
         act[u] = have_cur && seg < nseg;
         start[u] = seg == 0 ? (int)p.first_start : (int)gap_nib(gw[u], p.gap_nib0 + seg - 1u);
-        uint32_t la = w4[u];
-        if (GH_TILE_W4DPP) {
-          // segment seg + 1's first dword is the next lane's w.x (wave_shl:1; lane 63 keeps
-          // the uniform load, and so does the shard's last segment, whose look-ahead is
-          // the zero padding past it)
-          const uint32_t nx = (uint32_t)__builtin_amdgcn_update_dpp((int)w4[u], (int)w[u].x, 0x130, 0xf, 0xf, false);
-          la = (lane == 63 || seg + 1u >= nseg) ? w4[u] : nx;
-        }
-        make_ewin(w[u], la, start[u], S, e[u]);
+        make_ewin(w[u], w4[u], start[u], S, e[u]);
       }
       TSTAMP(1);
-      // GH_TILE_EARLY: the next tile's loads right here, into the registers the windows
-      // were just built from, so they have the whole iteration to arrive (the prefix
-      // load issued mid-decode then waits behind them in the in-order vmcnt queue)
-      if (GH_TILE_EARLY) load(nxt);
-      // Decoded unconditionally: in the last iterations (no tile) every chain is inactive
-      // and the loop stops after one group (the loads were issued, clamped to the last
-      // tile).  A branch around the decode made the compiler zero the 24 output words
-      // before it every iteration, and merge at the scans a path on which the loads
-      // were not yet waited for: a vmcnt(0) after every decode, which also waited there
-      // for the mid-decode prefix load.  (GH_TILE_MERGEWAIT=0: the old branch.)
       if (GH_TILE_ABLATE & 1) {  // diagnostic build: no decode, 16 bytes per segment (wrong output)
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -816,109 +592,168 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE,
 #pragma unroll
           for (int k2 = 0; k2 < OW; ++k2) ow[u][k2] = e[u][k2 % 5];
         }
-        finish(0);
-      } else if (GH_TILE_MERGEWAIT || have_cur) {
-        decode_tile_grouped<GRP, U, OW, MINL>(e, start, act, ow, cnt, amask, laneoff, hook, finish);
+        mid();
+        gdone = (16 + GRP - 1) / GRP;
       } else {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          cnt[u] = 0;
-#pragma unroll
-          for (int k2 = 0; k2 < OW; ++k2) ow[u][k2] = 0;
-        }
-        finish(0);
+        gdone = decode_tile_grouped<GRP, U, OW, MINL>(e, start, act, ow, cnt, amask, laneoff, mid);
       }
     }
-    // wave scans of the counts, before the copy-out: placed after it, the compiler waited
-    // for every outstanding load and store (vmcnt(0)) in the middle of the scans
-    // (the U scans are independent: issued together, their DPP steps interleave without
-    // the wait states one scan alone needs; then one exec-masked block for the stores)
+    // The next tile's words, right after the decode (its windows are dead, so the
+    // registers are free; issued during the decode they raised its register peak past
+    // 128): they have the rest of the iteration (~6 K cycles) to arrive.  Issued after the
+    // copy-out instead they had ~3 K cycles, and the next decode waited ~1.3 K cycles for
+    // them.  They follow the prefix loads, whose waits therefore do not include them
+    // (vmcnt is one in-order queue).
+    if (!GH_TILE_LATEPF) load(nxt);
     TSTAMP(2);
-    uint32_t bpos[U], incl[U];
+    // ---- wave scans: the segments' offsets in the wave's piece, the piece's length -------
+    uint32_t bpos[U], wave_tot = 0;
 #pragma unroll
-    for (int u = 0; u < U; ++u) incl[u] = wave_incl_scan(cnt[u]);
-    if (lane == 63) {
+    for (int u = 0; u < U; ++u) bpos[u] = wave_incl_scan(cnt[u]);
 #pragma unroll
-      for (int u = 0; u < U; ++u) s_wsum[(par * U + u) * NWAVE_T + wid] = incl[u];
+    for (int u = 0; u < U; ++u) {
+      const uint32_t ct = (uint32_t)__builtin_amdgcn_readlane((int)bpos[u], 63);
+      bpos[u] += wave_tot - cnt[u];
+      wave_tot += ct;
     }
-#pragma unroll
-    for (int u = 0; u < U; ++u) bpos[u] = incl[u] - cnt[u];
+    // ---- arrival at tile k: the last wave to arrive publishes its aggregate ------------
+    uint32_t tile_total = 0;
+    if (have_cur) {
+      uint32_t old = 0;
+      if (lane == 0) {
+        s_tot[slot * NW + wid] = wave_tot;
+        asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=v"(old) : "v"(cnt_lds + 4u * slot), "v"(1u)
+                     : "memory");
+      }
+      const uint32_t arr = (uint32_t)__builtin_amdgcn_readfirstlane((int)old);
+      rank = (4u * arr) / NW;
+      if (arr == NW - 1) {
+        // every wave's total of this tile is in LDS (each wave stored it before its add)
+        const uint32_t x = lane < NW ? s_tot[slot * NW + lane] : 0u;
+        const uint32_t xi = wave_incl_scan(x);
+        if (lane < NW) s_off[slot * NW + lane] = xi - x;
+        tile_total = (uint32_t)__builtin_amdgcn_readlane((int)xi, NW - 1);
+        if (lane == 0) {
+          s_cnt[slot] = 0;
+          // the offsets are in LDS before the aggregate leaves (a wave reads them once the
+          // prefix this aggregate leads to has arrived)
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __hip_atomic_store(&p.granules[cur], granule(p.epoch, 1, tile_total), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+#if GH_TILE_STAMPS
+          p.tstamps[cur] = __builtin_amdgcn_s_memrealtime();  // tile cur's aggregate left
+#endif
+        }
+      }
+    }
     TSTAMP(3);
-    // ---- copy tile k-2 out (its prefix was published about an iteration ago) ----------
-    // (one call site of load(nxt), after the prefix check: with a call in each branch the
-    // compiler hoisted the loads above the check, whose vmcnt(0) then waited for them)
-    if (!GH_TILE_IOVL) prefix_check();
+    // ---- the prefix of tile k-2 -> this wave's piece's output offset -------------------
+    unsigned long long goff = 0;
+    uint32_t n2 = 0;
+    if (have2 && (GH_TILE_ABLATE & 4)) {
+      goff = ((unsigned long long)t2 * (U * TB * 16) + (uint32_t)wid * (U * 64 * 16)) % (p.out_cap - (U * TB * 32));
+      n2 = s_tot[slot2 * NW + wid];
+    } else if (have2) {
+      // The wave's own early loads (top of the iteration, mid-decode) when they already
+      // show the prefix; else the LDS post of the first wave of the workgroup that saw it,
+      // or the wave's own poll, whichever comes first (the poll posts what it finds).
+      unsigned long long g = rfl_u64(gp0);  // wave-uniform: each waits for its own load only
+      bool polled = false, got = true;
+      if (!granule_ok(p, g, 2)) {
+        g = rfl_u64(gp);
+        if (!granule_ok(p, g, 2)) {
+          polled = true;
+          if (wid == 0 && lane == 0) atomicAdd(p.stats, 1ull);
+          unsigned long long t0w = 0;
+          for (uint32_t spins = 1;; ++spins) {
+            if (lds_ld_u32(ptile_lds + 4u * slot2) == t2) {
+              asm volatile("" ::: "memory");
+              g = s_pfx[slot2];
+              break;
+            }
+            g = rfl_u64(__hip_atomic_load(pf2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            if (granule_ok(p, g, 2)) {
+              if (lane == 0) {  // post: the value, then its tile (LDS order)
+                s_pfx[slot2] = g;
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                lds_st_u32(ptile_lds + 4u * slot2, t2);
+              }
+              break;
+            }
+            if ((spins & 63u) == 0u) {  // bounded like poll_granule: 4 s of the 100 MHz clock
+              if (__hip_atomic_load(p.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & GH_ST_TIMEOUT) break;
+              const unsigned long long t = wall_clock64();
+              if (t0w == 0) {
+                t0w = t;
+              } else if (t - t0w > 400000000ull) {
+                if (lane == 0) atomicOr(p.status, (unsigned)GH_ST_TIMEOUT);
+                break;
+              }
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+          got = granule_ok(p, g, 2);  // false only after a timeout (then nothing is written)
+        }
+      }
+      // the tile's offsets were in LDS before its aggregate left, and the aggregate before
+      // its prefix: read them only now (no compiler hoisting above the check)
+      asm volatile("" ::: "memory");
+      goff = (g & GRAN_VMASK) + s_off[slot2 * NW + wid];
+      n2 = s_tot[slot2 * NW + wid];
+      if (wid == NW - 1 && t2 == p.ntiles - 1 && got && lane == 0) *p.total = goff + n2;
+      ahead = polled;
+#if GH_TILE_STAMPS
+      if (wid == 0 && lane == 0) p.tstamps[p.ntiles + t2] = __builtin_amdgcn_s_memrealtime() | ((unsigned long long)polled << 63);
+#endif
+      n2 = (!got || goff >= p.out_cap) ? 0u : (uint32_t)min<unsigned long long>(n2, p.out_cap - goff);
+    }
+    if (GH_TILE_LATEPF) load(nxt);
     TSTAMP(4);
-    if (!GH_TILE_EARLY && !GH_TILE_IOVL) load(nxt);  // the next tile's words, issued before this copy-out's stores
-    // Unconditional (no tile two iterations back: n2 = 0, every store goes to the thread's
-    // junk slot): the same store count on every path lets the compiler wait for the
-    // prefetched loads with a counted vmcnt at the top of the next iteration.
-    if (!(GH_TILE_ABLATE & 8) && !GH_TILE_IOVL)
-      copy_out_tile<TB, TILE_NS, !GH_TILE_NOTAIL>(p.out, p.lut_bytes + buf * p.stage_bytes, goff,
-                                                   n2, tid,
-                                                   p.junk + (unsigned long long)blockIdx.x * TB + tid);
+    // ---- copy this wave's piece of tile k-2 out ------------------------------------------
+    // Unconditional (nothing to copy: n2 = 0, every store dropped): the same store count
+    // on every path lets the compiler wait for the prefetched loads with a counted vmcnt
+    // at the top of the next iteration.
+    if (!(GH_TILE_ABLATE & 8)) copy_out_piece<TILE_NS>(p.out, region0 + buf * NW * p.stage_bytes, goff, n2, lane);
     TSTAMP(5);
-    __syncthreads();  // tile sums
-    TSTAMP(6);
-    // the U x NWAVE_T wave sums in chain-then-wave order, one per lane, scanned with DPP:
-    // wave w's chain-u segments start at the exclusive prefix of entry u * NWAVE_T + w
-    static_assert(U * NWAVE_T <= 64, "one wave sum per lane");
-    const uint32_t xs = lane < U * NWAVE_T ? s_wsum[par * U * NWAVE_T + lane] : 0u;
-    const uint32_t xi = wave_incl_scan(xs);
-#pragma unroll
-    for (int u = 0; u < U; ++u) bpos[u] += (uint32_t)__builtin_amdgcn_readlane((int)(xi - xs), u * NWAVE_T + wid);
-    const uint32_t tile_total = (uint32_t)__builtin_amdgcn_readlane((int)xi, U * NWAVE_T - 1);
-    if (tid == 0 && have_cur)
-      __hip_atomic_store(&p.granules[cur], granule(p.epoch, 1, tile_total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // staging holds a tile of up to stage_bytes - STAGE_PAD - 48 bytes (sized for the
-    // typical tile, not the worst case: see tile_setup); a larger tile waits for its own
-    // prefix here and stores its bytes straight from registers
-    const bool staged = have_cur && tile_total + (uint32_t)(STAGE_PAD + 48) <= p.stage_bytes;
+    // ---- stage this tile's piece (copied out two iterations later) ----------------------
+    // a piece larger than the region (data whose shortest codewords cluster) waits for
+    // the tile's prefix instead and stores its bytes straight from registers (it has
+    // published its arrival, so the prefix cannot depend on it)
+    const bool staged = have_cur && wave_tot <= piece_cap;
     if (have_cur && !staged) {
-      unsigned long long goff = 0;
+      unsigned long long goffc = 0;
       bool got = true;
       if (lane == 0) {
         unsigned long long g = __hip_atomic_load(&p.prefix[cur], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (!granule_ok(p, g, 2)) g = poll_granule(p, &p.prefix[cur], 2);
         got = granule_ok(p, g, 2);  // false only after a timeout (then nothing is written)
-        goff = g & GRAN_VMASK;
-        if (wid == 0 && cur == p.ntiles - 1 && got) *p.total = goff + tile_total;
+        asm volatile("" ::: "memory");
+        goffc = (g & GRAN_VMASK) + s_off[slot * NW + wid];
+        if (wid == NW - 1 && cur == p.ntiles - 1 && got) *p.total = goffc + wave_tot;
       }
-      goff = rfl_u64(goff);
+      goffc = rfl_u64(goffc);
       if (__builtin_amdgcn_readfirstlane(got ? 1 : 0)) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) store_direct(p.out, p.out_cap, goff + bpos[u], ow[u], cnt[u]);
+        for (int u = 0; u < U; ++u) store_direct(p.out, p.out_cap, goffc + bpos[u], ow[u], cnt[u]);
       }
       // (rare path) drain its data-dependent loads and stores here, so that the
       // compiler's wait for the next tile's loads stays a counted vmcnt on the common path
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-    } else if (have_cur) {
-      // stage this tile into buffer k & 1 (copied out two iterations later) at its
-      // absolute LDS address (the kernel's LDS starts at 0)
-      const uint32_t sbase = p.lut_bytes + buf * p.stage_bytes + STAGE_PAD;
-      uint32_t nb[U], hv[U], ha[U];
+    } else if (have_cur && !(GH_TILE_ABLATE & 2)) {
+      const uint32_t sbase = region0 + buf * NW * p.stage_bytes + STAGE_PAD;
+      uint32_t o[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        nb[u] = 0;
-        hv[u] = ow[u][0];
-        ha[u] = sbase + bpos[u];
-        // a kept segment spans >= 113 bits, so it holds >= ceil(113 / maxlen) codewords
-        // (>= 12 when GRP >= 3, >= 10 otherwise; the stream's last segment may hold fewer,
-        // and its extra dwords land in the staging margin behind the tile)
-        constexpr int MINW = GH_TILE_P1MIN ? (GRP >= 3 ? 3 : 2) : 0;
-        if (cnt[u] && !(GH_TILE_ABLATE & 2)) nb[u] = stage_aligned_p1<OW, MINW>(ow[u], cnt[u], ha[u]);
-      }
-      TSTAMP(7);
-      __syncthreads();  // phase 1 done: every segment's tail dword is in place
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (nb[u]) stage_head(ha[u], hv[u], nb[u]);
+      for (int u = 0; u < U; ++u) o[u] = sbase + bpos[u];
+      // no segment of the wave holds more than GRP * gdone codewords: rounds above its
+      // last dword are skipped
+      stage_wave<U, OW>(ow, cnt, o, min(OW, (GRP * gdone + 3) >> 2));
     }
+    TSTAMP(6);
 #if GH_TILE_STAMPS
+    TSTAMP(7);
     TSTAMP(8);
-    if (!(have_cur && staged)) ts[7] = ts[8];
-    if (lane == 0 && (wid & 3) == 0 && k < 128) {
-      uint4* st = p.stamps + (((unsigned long long)blockIdx.x * 2 + (wid >> 2)) * 128 + k) * 2;
+    if (lane == 0 && (wid == 0 || wid == NW / 2) && k < 128) {  // the first wave of each half
+      uint4* st = p.stamps + (((unsigned long long)blockIdx.x * 2 + (wid ? 1 : 0)) * 128 + k) * 2;
       st[0] = make_uint4((uint32_t)(ts[1] - ts[0]), (uint32_t)(ts[2] - ts[1]), (uint32_t)(ts[3] - ts[2]),
                          (uint32_t)(ts[4] - ts[3]));
       st[1] = make_uint4((uint32_t)(ts[5] - ts[4]), (uint32_t)(ts[6] - ts[5]), (uint32_t)(ts[7] - ts[6]),
@@ -926,10 +761,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(GH_TILE_WPE,
     }
 #endif
     t2 = t1;
-    tot2 = tot1;
     t1 = staged ? cur : NONE;
-    tot1 = tile_total;
-    buf ^= 1u;
     cur = nxt < p.ntiles ? nxt : NONE;
     nxt += G;
   }

@@ -11,7 +11,8 @@
 #   cmp WL[,WL] LIB...        cmp_libs.py: build variants side by side (LIB = base | name[@VAR=v...])
 #   bench NAME [ARGS...]      bench.py ARGS --out-json OUT/NAME.json
 #   stats NAME WL             rocprofv3 --kernel-trace --stats of quick_one.py WL
-#   sq NAME WL                two SQ counter passes (issue / wait / LDS) of quick_one.py WL
+#   sq NAME WL [LIB]          two SQ counter passes (issue / wait / LDS) of quick_one.py WL
+#                             (LIB: a build variant's name, lib/libgaphuff_LIB.so)
 #   traffic NAME WL           FETCH_SIZE and WRITE_SIZE passes (separate runs)
 #   cmd NAME SECS CMD...      anything else, under its own time limit
 # WL: cfg2 | cfg3 | cfg4 | cfg5 | name:N:r.  Every step runs under its own `timeout -k`;
@@ -73,13 +74,15 @@ for spec in "$@"; do
       f=$(find "$O/stats_${a[1]}" -name '*kernel_stats.csv' | head -1)
       [ -n "$f" ] && cp "$f" "$O/${a[1]}_kernel_stats.csv" && cat "$O/${a[1]}_kernel_stats.csv" ;;
     sq)
+      if [ -n "${a[3]}" ]; then export GAPHUFF_LIB=$PWD/cse375-finalproj-huffman-decoding_amd/lib/libgaphuff_${a[3]}.so; fi
       i=1
       for set in "$SQ1" "$SQ2"; do
         step "sq$i-${a[1]}" 150 "$O/sq${i}_${a[1]}.log" timeout -s KILL 120 rocprofv3 --pmc $set --kernel-trace \
           --output-format csv -d "$O/sq${i}_${a[1]}" -o run -- python3 scripts/quick_one.py "$(wl "${a[2]}")" 5 || exit 1
         python3 scripts/pmc_summary.py "$O/sq${i}_${a[1]}" | tee -a "$O/sq_${a[1]}.txt"
         i=$((i + 1))
-      done ;;
+      done
+      unset GAPHUFF_LIB ;;
     traffic)
       for c in FETCH_SIZE WRITE_SIZE; do
         step "pmc-$c-${a[1]}" 150 "$O/pmc_${c}_${a[1]}.log" timeout -s KILL 120 rocprofv3 --pmc $c --kernel-trace \

@@ -17,9 +17,9 @@ r = subprocess.run([sys.executable, os.path.join(here, "quick_one.py"), wl, "3"]
 print(r.stdout.strip(), r.stderr.strip()[-500:])
 a = np.fromfile(out, dtype=np.uint32)
 os.unlink(out)
-grid = a.size // (2 * 128 * 8)
-a = a.reshape(grid, 2, 128, 8).astype(np.float64)
-names = ["load wait", "decode", "scans", "prefix", "copy-out", "barrier 1", "publish+stage1", "barrier 2+stage2"]
+grid = int(dict(x.split("=", 1) for x in r.stdout.split() if "=" in x)["grid"])
+a = a[:grid * 2 * 128 * 8].reshape(grid, 2, 128, 8).astype(np.float64)  # (then the chain times)
+names = ["load wait", "decode", "scans+arrive", "prefix", "copy-out", "stage", "-", "-"]
 valid = a.sum(axis=3) > 0
 valid[0] = False  # workgroup 0 leads the rounds
 print(f"grid {grid}, stamped iterations {int(valid.sum())}")
@@ -47,3 +47,17 @@ print("per-WG prefix cycles", np.percentile(pref[sel], q).round(-3))
 slow = np.argsort(busy[sel])[-8:]
 print("slowest WGs (busy)  ", np.nonzero(sel)[0][slow], busy[sel][slow].round(-3))
 
+# by XCD (blocks are dealt round-robin over the 8 XCDs: block b on XCD b mod 8, as
+# observed; which physical XCD is not fixed) and, for the slowest / fastest workgroups,
+# the phases that differ
+blk = np.arange(grid)
+for x in range(8):
+    m = sel & (blk % 8 == x)
+    if m.any():
+        ph = (w0[m].sum(axis=1) / iters[m][:, None]).mean(axis=0)
+        print(f"XCD {x}: busy/iter {(busy[m] / iters[m]).mean():7.0f}  " +
+              "  ".join(f"{n} {ph[i]:6.0f}" for i, n in enumerate(names[:6])))
+for label, idx in [("slowest 8", np.nonzero(sel)[0][np.argsort(busy[sel])[-8:]]),
+                   ("fastest 8", np.nonzero(sel)[0][np.argsort(busy[sel])[:8]])]:
+    ph = (w0[idx].sum(axis=1) / iters[idx][:, None]).mean(axis=0)
+    print(f"{label}: " + "  ".join(f"{n} {ph[i]:6.0f}" for i, n in enumerate(names[:6])))
