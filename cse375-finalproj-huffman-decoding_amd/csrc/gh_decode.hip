@@ -230,7 +230,7 @@ static int tile_setup(gh_ctx* c, uint32_t K, double avg_seg_bytes) {
     }
   if (c->grid < 2) return GH_OK;  // (the wave split then takes the code)
   if (GH_TILE_STAMPS) {
-    const size_t nb = 32ull * c->grid * 2 * 128 + 8ull * (2ull * c->ntiles + c->ntiles + 64);
+    const size_t nb = 32ull * c->grid * 2 * 128 + 8ull * (3ull * c->ntiles + 64 + 4 * 1024);
     GH_HIP(hipMalloc(&c->d_stamps, nb));
     GH_HIP(hipMemset(c->d_stamps, 0, nb));
   }
@@ -765,7 +765,7 @@ extern "C" int gh_ctx_report(gh_ctx* c, void* hip_stream, gh_report* rep) {
   c->pending.clear();
   if (GH_TILE_STAMPS && c->d_stamps) {  // diagnostic builds: the last decode's phase deltas
     if (const char* f = getenv("GH_STAMPS_OUT")) {
-      std::vector<uint8_t> h(32ull * c->grid * 2 * 128 + 8ull * (3ull * c->ntiles + 64));
+      std::vector<uint8_t> h(32ull * c->grid * 2 * 128 + 8ull * (3ull * c->ntiles + 64 + 4 * 1024));
       GH_HIP(hipMemcpy(h.data(), c->d_stamps, h.size(), hipMemcpyDeviceToHost));
       if (FILE* fp = fopen(f, "wb")) {
         fwrite(h.data(), 1, h.size(), fp);

@@ -12,8 +12,8 @@
 //
 //   decode tile k into registers (one codeword per lookup, G codewords per window shift;
 //     a codeword is kept iff it starts before the segment end: the reference's rule)
-//     - mid-decode: load the global prefix of tile k-2
-//   copy tile k-2 out of staging (its prefix has had an iteration to arrive), with a
+//     - mid-decode: load the global prefix of tile k-LAG
+//   copy tile k-LAG out of staging (its prefix has had LAG-1 iterations to arrive), with a
 //     fixed store count; the next tile's loads are issued just before
 //   wave scans of the counts -> BARRIER -> publish tile k's aggregate
 //   stage tile k: every wave writes its own 64U segments (no second barrier, below); a
@@ -42,9 +42,13 @@ constexpr int TILE_U = 3;     // segments per lane, codes of >= 4-bit codewords
 constexpr int TILE_U3 = 2;    // segments per lane, codes with 3-bit codewords
 constexpr int TILE_NS = 4;    // 16-byte stores per lane per copy-out (NS * 64 chunks cover a wave's piece)
 constexpr int TILE_SCAP = 20; // staging bytes per segment, codes of >= 4-bit codewords
-constexpr int TILE_MIDG = 2;  // decode group after which the prefix of tile k-2 is loaded (again)
+constexpr int TILE_MIDG = 2;  // decode group after which the prefix of tile k-LAG is loaded (again)
 constexpr int STAGE_PAD = 16; // region byte STAGE_PAD + i = piece byte i
-constexpr int TILE_SLOTS = 8; // per-tile wave totals / offsets / arrival counters in LDS, by k mod 8
+#ifndef GH_TILE_LAG
+#define GH_TILE_LAG 2
+#endif
+constexpr int TILE_LAG = GH_TILE_LAG;  // a tile is copied out LAG iterations after it is decoded (LAG buffers)
+constexpr int TILE_SLOTS = 16;  // per-tile wave totals / offsets / arrival counters / prefixes in LDS, by k mod 16
 #ifndef GH_TILE_STAMPS
 #define GH_TILE_STAMPS 0  // diagnostic builds only: per-phase s_memtime deltas of waves 0 and 4
 #endif
@@ -95,7 +99,7 @@ struct TileParams {
 // per-tile wave totals, offsets and arrival counters (TILE_SLOTS tiles), leader wave totals.
 // stage_bytes: one wave's region.
 inline size_t tile_lds_bytes(size_t lut_bytes, size_t stage_bytes) {
-  return lut_bytes + 2 * (TILE_TB / 64) * stage_bytes + TILE_SLOTS * (2 * (TILE_TB / 64) + 1) * 4 +
+  return lut_bytes + TILE_LAG * (TILE_TB / 64) * stage_bytes + TILE_SLOTS * (2 * (TILE_TB / 64) + 1) * 4 +
          TILE_SLOTS * 12 + 4 * (TILE_TB / 64) + 32;
 }
 
@@ -459,7 +463,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
   constexpr int NW = TB / 64;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t stage_lds = p.lut_bytes;                                  // [2][NW] regions
-  uint32_t* s_tot = (uint32_t*)(smem + p.lut_bytes + 2 * NW * p.stage_bytes);  // [SLOTS][NW] wave totals
+  uint32_t* s_tot = (uint32_t*)(smem + p.lut_bytes + TILE_LAG * NW * p.stage_bytes);  // [SLOTS][NW] wave totals
   uint32_t* s_off = s_tot + TILE_SLOTS * NW;                                // [SLOTS][NW] wave offsets
   uint32_t* s_cnt = s_off + TILE_SLOTS * NW;                                // [SLOTS] arrivals
   unsigned long long* s_pfx = (unsigned long long*)(s_cnt + TILE_SLOTS);   // [SLOTS] prefixes (wave 0)
@@ -469,10 +473,25 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
   const uint32_t ptile_lds = (uint32_t)((uint8_t*)s_ptile - smem);
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+#if GH_TILE_STAMPS
+  // per launch (ring of 1024 by epoch): shader-clock and 100 MHz times at the leader's start
+  // and end, to read the clock the kernel ran at
+  unsigned long long* const lring = p.tstamps + 3ull * p.ntiles + 64 + 4ull * (p.epoch & 1023u);
+  if (blockIdx.x == 0 && tid == 0) {
+    lring[0] = __builtin_amdgcn_s_memtime();
+    lring[1] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
   // decoding workgroups: every block but 0 (the leader) and p.idle_block (if < grid)
   const uint32_t D = gridDim.x - 1 - (p.idle_block < gridDim.x ? 1u : 0u);
   if (blockIdx.x == 0) {
     tile_round_leader<TB>(p, D, s_lead, tid, lane, wid);
+#if GH_TILE_STAMPS
+    if (tid == 0) {
+      lring[2] = __builtin_amdgcn_s_memtime();
+      lring[3] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
     return;
   }
   if (blockIdx.x == p.idle_block) return;  // the leader's CU partner (GH_TILE_IDLE): no decoding
@@ -522,7 +541,9 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     __builtin_amdgcn_raw_buffer_store_b8((uint8_t)0, rs, (int)OOB_OFF, 0, 2);
   }
   if (cur >= p.ntiles) cur = NONE;
-  uint32_t t1 = NONE, t2 = NONE;  // this wave's pieces of iterations k-1, k-2 (NONE: not staged)
+  uint32_t th[TILE_LAG];          // this wave's pieces of iterations k-1 .. k-LAG (NONE: not staged)
+#pragma unroll
+  for (int i = 0; i < TILE_LAG; ++i) th[i] = NONE;
   bool ahead = false;             // the last prefix had to be polled
   uint32_t rank = 0;              // (GH_TILE_RANKPRIO) the wave's arrival rank at its last tile, in quarters
   const uint32_t region0 = stage_lds + (uint32_t)wid * p.stage_bytes;  // buffer 0; buffer 1 at + NW * stage_bytes
@@ -533,14 +554,18 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
   for (uint32_t k = 0;; ++k) {
     TSTAMP(0);
     const bool have_cur = cur < p.ntiles;
-    const bool have2 = t2 < p.ntiles;  // this wave's piece of tile k-2 is copied out this iteration
-    if (!have_cur && t1 >= p.ntiles && !have2) break;
-    if (last_tile_k != NONE && k > last_tile_k + 4) {  // cannot happen; never hang the GPU
+    const uint32_t t2 = th[TILE_LAG - 1];  // the piece copied out this iteration (tile k - LAG)
+    const bool have2 = t2 < p.ntiles;
+    bool pending = have_cur;
+#pragma unroll
+    for (int i = 0; i < TILE_LAG; ++i) pending |= th[i] < p.ntiles;
+    if (!pending) break;
+    if (last_tile_k != NONE && k > last_tile_k + TILE_LAG + 2) {  // cannot happen; never hang the GPU
       if (lane == 0) atomicOr(p.status, (unsigned)GH_ST_TIMEOUT);
       break;
     }
-    const uint32_t slot = k % TILE_SLOTS, slot2 = (k + TILE_SLOTS - 2) % TILE_SLOTS;
-    const uint32_t buf = k & 1u;
+    const uint32_t slot = k % TILE_SLOTS, slot2 = (k + TILE_SLOTS - TILE_LAG) % TILE_SLOTS;
+    const uint32_t buf = k % TILE_LAG;
     if (GH_TILE_RANKPRIO) {
       // by the wave's arrival rank at its last tile (0: first of the workgroup's waves):
       // the waves that arrive last gate the tile's aggregate, so they issue first
@@ -553,7 +578,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     } else {
       __builtin_amdgcn_s_setprio(2);
     }
-    // prefix of tile k-2 (lane 0): loaded at the top and again mid-decode; the first that
+    // prefix of tile k-LAG: loaded at the top and again mid-decode; the first that
     // shows it published is used (a load at the top alone often saw it a little before it
     // was published, and the re-poll then paid a full memory round trip)
     // (every lane loads the same word, one request; no branch around the load: the
@@ -647,7 +672,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
       }
     }
     TSTAMP(3);
-    // ---- the prefix of tile k-2 -> this wave's piece's output offset -------------------
+    // ---- the prefix of tile k-LAG -> this wave's piece's output offset -------------------
     unsigned long long goff = 0;
     uint32_t n2 = 0;
     if (have2 && (GH_TILE_ABLATE & 4)) {
@@ -709,13 +734,13 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     }
     if (GH_TILE_LATEPF) load(nxt);
     TSTAMP(4);
-    // ---- copy this wave's piece of tile k-2 out ------------------------------------------
+    // ---- copy this wave's piece of tile k-LAG out ----------------------------------------
     // Unconditional (nothing to copy: n2 = 0, every store dropped): the same store count
     // on every path lets the compiler wait for the prefetched loads with a counted vmcnt
     // at the top of the next iteration.
     if (!(GH_TILE_ABLATE & 8)) copy_out_piece<TILE_NS>(p.out, region0 + buf * NW * p.stage_bytes, goff, n2, lane);
     TSTAMP(5);
-    // ---- stage this tile's piece (copied out two iterations later) ----------------------
+    // ---- stage this tile's piece (copied out LAG iterations later) ----------------------
     // a piece larger than the region (data whose shortest codewords cluster) waits for
     // the tile's prefix instead and stores its bytes straight from registers (it has
     // published its arrival, so the prefix cannot depend on it)
@@ -760,8 +785,9 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
                          (uint32_t)(ts[8] - ts[7]));
     }
 #endif
-    t2 = t1;
-    t1 = staged ? cur : NONE;
+#pragma unroll
+    for (int i = TILE_LAG - 1; i > 0; --i) th[i] = th[i - 1];
+    th[0] = staged ? cur : NONE;
     cur = nxt < p.ntiles ? nxt : NONE;
     nxt += G;
   }
