@@ -38,7 +38,10 @@
 #define GH_TILE_TB 1024
 #endif
 constexpr int TILE_TB = GH_TILE_TB;  // threads per workgroup
-constexpr int TILE_U = 3;     // segments per lane, codes of >= 4-bit codewords
+#ifndef GH_TILE_U
+#define GH_TILE_U 3
+#endif
+constexpr int TILE_U = GH_TILE_U;  // segments per lane, codes of >= 4-bit codewords
 constexpr int TILE_U3 = 2;    // segments per lane, codes with 3-bit codewords
 constexpr int TILE_NS = 4;    // 16-byte stores per lane per copy-out (NS * 64 chunks cover a wave's piece)
 constexpr int TILE_SCAP = 20; // staging bytes per segment, codes of >= 4-bit codewords
@@ -56,6 +59,12 @@ constexpr int TILE_SLOTS = 16;  // per-tile wave totals / offsets / arrival coun
 #define TSTAMP(i) (ts[i] = __builtin_amdgcn_s_memtime())
 #else
 #define TSTAMP(i) ((void)0)
+#endif
+#ifndef GH_TILE_ROLL
+#define GH_TILE_ROLL 0  // the decode's chains rolling (decode_tile_rolling) instead of in lock-step
+#endif
+#ifndef GH_TILE_CBORROW
+#define GH_TILE_CBORROW 0  // the decode's borrow count in C instead of inline asm
 #endif
 #ifndef GH_TILE_RANKPRIO
 #define GH_TILE_RANKPRIO 1  // issue priority by arrival rank (0: by "had to poll", the round-3/4 rule)
@@ -177,10 +186,17 @@ __device__ __forceinline__ int decode_tile_grouped(uint32_t (&e)[U][5], const in
         }
         lds_wait(ent);
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-          asm("v_sub_co_u32 %0, vcc, %0, %2\n\t"
-              "v_cndmask_b32_e64 %1, %1, %3, vcc"
-              : "+v"(q[u]), "+v"(cnt[u]) : "v"(ent[u]), "i"(pos + 1) : "vcc");
+        for (int u = 0; u < U; ++u) {
+          if (GH_TILE_CBORROW) {  // the compiler's v_sub_co_u32 + v_cndmask (no asm boundaries)
+            const bool borrow = q[u] < ent[u];
+            q[u] -= ent[u];
+            cnt[u] = borrow ? (uint32_t)(pos + 1) : cnt[u];
+          } else {
+            asm("v_sub_co_u32 %0, vcc, %0, %2\n\t"
+                "v_cndmask_b32_e64 %1, %1, %3, vcc"
+                : "+v"(q[u]), "+v"(cnt[u]) : "v"(ent[u]), "i"(pos + 1) : "vcc");
+          }
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u)
           ow[u][pos >> 2] = __builtin_amdgcn_perm(ent[u], ow[u][pos >> 2], perm_sel(pos & 3));
@@ -208,6 +224,100 @@ __device__ __forceinline__ int decode_tile_grouped(uint32_t (&e)[U][5], const in
     // (no exit before mid(): every path then issues its loads at the same point, which
     // keeps the compiler's wait counts exact; every kept segment runs past group MIDG)
     if (gi >= TILE_MIDG && gi + 1 < NG && !__any(qmin < Q_LIVE)) {
+      gdone = gi + 1;
+      break;
+    }
+  }
+  return gdone;
+}
+
+// Wait until at most N LDS operations of the wave are outstanding (they complete in
+// order), tied to v so the compiler uses it only after the wait.
+template <int N>
+__device__ __forceinline__ void lds_wait_n(uint32_t& v) {
+  static_assert(N >= 0 && N <= 3, "lgkmcnt 0..3");
+  if constexpr (N == 0) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v)::"memory");
+  else if constexpr (N == 1) asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(v)::"memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(v)::"memory");
+  else asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(v)::"memory");
+}
+
+// The same decode with the chains' lookups rolling: each chain waits only for its own
+// read (a counted lgkmcnt: LDS reads of a wave complete in order) and issues its next
+// one at once, so U reads stay in flight and a chain's step costs one LDS round trip plus
+// its own few ops (decode_tile_grouped waits for all U reads, then processes all U).
+// A chain shifts its window at its own group end; the early exit, after a group of every
+// chain, drains the next group's U reads.
+template <int G, int U, int OW, int MINL, class Mid>
+__device__ __forceinline__ int decode_tile_rolling(uint32_t (&e)[U][5], const int (&start)[U], const bool (&act)[U],
+                                                   uint32_t (&ow)[U][OW], uint32_t (&cnt)[U], uint32_t amask,
+                                                   uint32_t laneoff, Mid&& mid) {
+  constexpr int S = 4 * OW;
+  constexpr int NG = (S + G - 1) / G;
+  uint32_t q[U], ent[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    q[u] = q_init(act[u], start[u]);
+    cnt[u] = 0;
+#pragma unroll
+    for (int k = 0; k < OW; ++k) asm volatile("" : "=v"(ow[u][k]));
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) ent[u] = lds_u32_nowait((e[u][0] & amask) | laneoff);
+  int gdone = NG;
+#pragma clang loop unroll(full)
+  for (int gi = 0; gi < NG; ++gi) {
+    const int CMIN = (gi + 1) * G * MINL;  // bits consumed by the end of this group, at least
+    uint32_t qmin = 0xFFFFFFFFu;
+#pragma clang loop unroll(full)
+    for (int j = 0; j < G; ++j) {
+      const int pos = gi * G + j;
+      if (pos < S) {
+        const bool gend = (j == G - 1) || (pos + 1 >= S);  // this chain's last codeword of the group
+        const bool last = gend && gi + 1 >= NG;             // no read after it
+#pragma clang loop unroll(full)
+        for (int u = 0; u < U; ++u) {
+          // outstanding: chains u.. of this codeword, and chains ..u-1's next reads
+          if (last) {
+            if constexpr (U == 3) {
+              if (u == 0) lds_wait_n<2>(ent[u]);
+              else if (u == 1) lds_wait_n<1>(ent[u]);
+              else lds_wait_n<0>(ent[u]);
+            } else if constexpr (U == 2) {
+              if (u == 0) lds_wait_n<1>(ent[u]);
+              else lds_wait_n<0>(ent[u]);
+            } else {
+              lds_wait_n<0>(ent[u]);
+            }
+          } else {
+            lds_wait_n<U - 1>(ent[u]);
+          }
+          asm("v_sub_co_u32 %0, vcc, %0, %2\n\t"
+              "v_cndmask_b32_e64 %1, %1, %3, vcc"
+              : "+v"(q[u]), "+v"(cnt[u]) : "v"(ent[u]), "i"(pos + 1) : "vcc");
+          ow[u][pos >> 2] = __builtin_amdgcn_perm(ent[u], ow[u][pos >> 2], perm_sel(pos & 3));
+          if (!gend) {
+            const uint32_t x = __builtin_amdgcn_alignbit(e[u][0], e[u][1], q[u]);
+            ent[u] = lds_u32_nowait((x & amask) | laneoff);
+          } else {
+            // window shift (see decode_tile_grouped for the trim of words no kept codeword reads)
+            e[u][0] = __builtin_amdgcn_alignbit(e[u][0], e[u][1], q[u]);
+            if (CMIN + 32 < 157) e[u][1] = __builtin_amdgcn_alignbit(e[u][1], e[u][2], q[u]);
+            if (CMIN + 64 < 157) e[u][2] = __builtin_amdgcn_alignbit(e[u][2], e[u][3], q[u]);
+            if (CMIN + 96 < 157) e[u][3] = __builtin_amdgcn_alignbit(e[u][3], e[u][4], q[u]);
+            if (CMIN + 128 < 157) e[u][4] = __builtin_amdgcn_alignbit(e[u][4], 0u, q[u]);
+            q[u] = (q[u] & 0xFFFFFF00u) | 32u;
+            qmin = min(qmin, q[u]);
+            if (!last) ent[u] = lds_u32_nowait((e[u][0] & amask) | laneoff);
+          }
+        }
+      }
+    }
+    if (gi == TILE_MIDG) mid();
+    if (gi >= TILE_MIDG && gi + 1 < NG && !__any(qmin < Q_LIVE)) {
+      // the next group's reads are in flight: drain them
+#pragma unroll
+      for (int u = 0; u < U; ++u) lds_wait_n<0>(ent[u]);
       gdone = gi + 1;
       break;
     }
@@ -620,7 +730,8 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
         mid();
         gdone = (16 + GRP - 1) / GRP;
       } else {
-        gdone = decode_tile_grouped<GRP, U, OW, MINL>(e, start, act, ow, cnt, amask, laneoff, mid);
+        if (GH_TILE_ROLL) gdone = decode_tile_rolling<GRP, U, OW, MINL>(e, start, act, ow, cnt, amask, laneoff, mid);
+        else gdone = decode_tile_grouped<GRP, U, OW, MINL>(e, start, act, ow, cnt, amask, laneoff, mid);
       }
     }
     // The next tile's words, right after the decode (its windows are dead, so the

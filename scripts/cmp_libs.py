@@ -11,7 +11,7 @@ for wl in sys.argv[1].split(","):
         lib = os.path.join(libdir, f"libgaphuff{'' if name == 'base' else '_' + name}.so")
         env = dict(os.environ, GAPHUFF_LIB=lib, **dict(e.split("=", 1) for e in envs))
         try:
-            r = subprocess.run([sys.executable, os.path.join(here, "quick_one.py"), wl, "20"], env=env,
+            r = subprocess.run([sys.executable, os.path.join(here, "quick_one.py"), wl, os.environ.get("CMP_REPS", "20")], env=env,
                            capture_output=True, text=True, timeout=90)
         except subprocess.TimeoutExpired:
             print(f"{spec:10s} TIMEOUT (90 s)", flush=True)

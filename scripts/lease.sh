@@ -9,6 +9,7 @@
 #   smoke                     __graft_entry__.smoke()
 #   perf WL...                quick_one.py per workload (kernel ms, frac, bit-exact)
 #   cmp WL[,WL] LIB...        cmp_libs.py: build variants side by side (LIB = base | name[@VAR=v...])
+#   cmpss WL[,WL] LIB...      the same in the steady state (60 untimed + 100 timed decodes each)
 #   bench NAME [ARGS...]      bench.py ARGS --out-json OUT/NAME.json
 #   stats NAME WL             rocprofv3 --kernel-trace --stats of quick_one.py WL
 #   sq NAME WL [LIB]          two SQ counter passes (issue / wait / LDS) of quick_one.py WL
@@ -59,12 +60,14 @@ for spec in "$@"; do
         step "perf-$w" 300 "$O/perf_$w.log" python -u scripts/quick_one.py "$(wl "$w")" 20 || true
         cat "$O/perf_$w.log"
       done ;;
-    cmp)
+    cmp|cmpss)
+      if [ "$kind" = cmpss ]; then export QO_WARM=60 CMP_REPS=100; fi
       ws=""
       IFS=',' read -ra wls <<< "${a[1]}"
       for w in "${wls[@]}"; do ws="$ws${ws:+,}$(wl "$w")"; done
-      step cmp 900 "$O/cmp_${a[1]//,/_}.log" python -u scripts/cmp_libs.py "$ws" "${a[@]:2}" || true
-      cat "$O/cmp_${a[1]//,/_}.log" ;;
+      step "$kind" 900 "$O/${kind}_${a[1]//,/_}.log" python -u scripts/cmp_libs.py "$ws" "${a[@]:2}" || true
+      unset QO_WARM CMP_REPS
+      cat "$O/${kind}_${a[1]//,/_}.log" ;;
     bench)
       step "bench-${a[1]}" 600 "$O/bench_${a[1]}.err" python bench.py "${a[@]:2}" --out-json "$O/${a[1]}.json" || true
       cat "$O/${a[1]}.json" 2> /dev/null || tail -20 "$O/bench_${a[1]}.err" ;;
