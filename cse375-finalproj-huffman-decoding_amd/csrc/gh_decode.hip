@@ -39,6 +39,7 @@ constexpr uint32_t EPOCH_MAX = (1u << 24) - 1;
 
 #include "gh_tile.hip"
 #include "gh_wsplit.hip"
+#include "gh_mtile.hip"
 
 }  // namespace gh
 
@@ -64,6 +65,17 @@ static const void* tile_kernel_for(uint32_t minlen, uint32_t g) {
   return g >= 4 ? (const void*)gh_tile_kernel<TILE_TB, TILE_U3, 4, 11, 3>
        : g == 3 ? (const void*)gh_tile_kernel<TILE_TB, TILE_U3, 3, 11, 3>
                 : (const void*)gh_tile_kernel<TILE_TB, TILE_U3, 2, 11, 3>;
+}
+
+// Two-pass tile kernel by lookups per window shift and 16-byte stores per copy-out.
+template <int GL>
+static const void* mtile_ns(int ns) {
+  return ns <= 4 ? (const void*)gh_mtile_kernel<MT_TB, GL, 4>
+       : ns <= 6 ? (const void*)gh_mtile_kernel<MT_TB, GL, 6>
+                 : (const void*)gh_mtile_kernel<MT_TB, GL, 8>;
+}
+static const void* mtile_kernel_for(int gl, int ns) {
+  return gl >= 4 ? mtile_ns<4>(ns) : gl == 3 ? mtile_ns<3>(ns) : mtile_ns<2>(ns);
 }
 
 struct WsKernels {
@@ -117,6 +129,8 @@ struct gh_ctx {
   uint32_t tile_k = 0, tile_g = 0, lgr = 0;  // LUT width, codewords per window shift, log2 LUT copies
   uint32_t tile_minl = 4, tile_u = TILE_U;     // kernel shape (tile_kernel_for), segments per lane
   uint32_t idle_block = 0xFFFFFFFFu;           // GH_TILE_IDLE experiments: a block that exits at once
+  bool mtile = false;              // the two-pass tile kernel (gh_mtile.hip; c->tile is set too)
+  int mt_gl = 2, mt_ns = 4;        // its lookups per window shift, stores per copy-out
   uint32_t* d_lut_t = nullptr;
   uint4* d_stamps = nullptr;       // GH_TILE_STAMPS builds only
   unsigned long long* d_gran = nullptr;  // granules, within-round prefixes, round starts
@@ -163,6 +177,7 @@ static void free_shard(gh_ctx* c) {
   c->d_rng_tot = nullptr;
   c->d_rng_off = nullptr;
   c->tile = false;
+  c->mtile = false;
   c->ws = false;
   c->loaded = false;
 }
@@ -234,6 +249,54 @@ static int tile_setup(gh_ctx* c, uint32_t K, double avg_seg_bytes) {
     GH_HIP(hipMalloc(&c->d_stamps, nb));
     GH_HIP(hipMemset(c->d_stamps, 0, nb));
   }
+  c->tile = true;
+  return GH_OK;
+}
+
+// ---- two-pass tile kernel setup (gh_mtile.hip) -------------------------------------
+// Codes for it: complete, 2 <= len <= 12 (at most 64 codewords per segment), not taken
+// by the single-pass tile kernel.  One LUT of width K (the wave split's write width) with
+// the codewords' start masks; one staging region per wave, sized for the stream's mean
+// bytes per segment + 12 % and at least one chain's worst case (64 x 64 bytes: a larger
+// piece is written and copied out chain by chain).  Returns GH_OK with c->tile false when
+// it does not fit a CU.
+static uint32_t ws_write_bits(const Canon& cn);
+static int mtile_setup(gh_ctx* c, double avg_seg_bytes) {
+  const Canon& cn = c->canon;
+  const uint32_t K = ws_write_bits(cn);
+  if (K < cn.maxlen) return GH_OK;
+  const uint32_t maxsyms = (128 + cn.minlen - 1) / cn.minlen;  // <= 64
+  double scapf = 1.12;
+  if (const char* e = getenv("GH_TILE_SCAPF")) scapf = std::clamp(atof(e), 0.5, 4.0);
+  uint64_t per_seg = std::min<uint64_t>(maxsyms, (uint64_t)std::ceil(std::max(avg_seg_bytes, 1.0) * scapf + 1));
+  if (const char* e = getenv("GH_TILE_SCAP")) per_seg = std::min<uint64_t>(maxsyms, (uint64_t)std::max(1, atoi(e)));
+  // at most what the LDS (LUT + 16 regions + slots) and the copy-out's 8 x 64 chunks hold
+  const uint64_t lds_free = 160ull * 1024 - (8ull << K) - mtile_lds_bytes(0, 0);
+  const uint64_t region_max = std::min<uint64_t>(lds_free / (MT_TB / 64), 8 * 1024 + STAGE_PAD) & ~15ull;
+  per_seg = std::min<uint64_t>(per_seg, (region_max - STAGE_PAD - 16) / (64ull * MT_U));
+  const uint64_t cap = std::max<uint64_t>(64ull * MT_U * per_seg, 64ull * maxsyms);  // piece bytes staged at once
+  if (STAGE_PAD + cap + 16 > region_max) return GH_OK;
+  c->mt_ns = cap + 16 <= 4096 ? 4 : cap + 16 <= 6144 ? 6 : 8;  // the copy-out's chunks cover a piece
+  c->stage_bytes = (uint32_t)((STAGE_PAD + cap + 16 + 15) & ~15ull);  // + the write overrun
+  c->mt_gl = lookups_per_shift(K);
+  const void* kern = mtile_kernel_for(c->mt_gl, c->mt_ns);
+  c->lut_bytes = 8ull << K;
+  c->lds = mtile_lds_bytes(c->lut_bytes, c->stage_bytes);
+  int pc = 0;
+  GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, kern, MT_TB, c->lds));
+  pc = std::min(pc, 2);  // (as tile_setup: the occupancy query can answer one too many)
+  if (pc < 1) return GH_OK;
+  const std::vector<uint64_t> lt = multi_lut(cn, K);
+  GH_HIP(hipMalloc(&c->d_lut_t, 8ull << K));
+  GH_HIP(hipMemcpy(c->d_lut_t, lt.data(), 8ull << K, hipMemcpyHostToDevice));
+  c->tile_k = K;
+  c->lgr = 0;
+  c->tile_u = MT_U;
+  c->ntiles = (uint32_t)ceil_div(c->nseg, (uint64_t)MT_U * MT_TB);
+  c->grid = (uint32_t)std::min<uint64_t>({(uint64_t)c->ntiles + 1, (uint64_t)pc * c->num_cu, (uint64_t)LEAD_A * MT_TB});
+  if (c->grid < 2) return GH_OK;
+  c->idle_block = 0xFFFFFFFFu;
+  c->mtile = true;
   c->tile = true;
   return GH_OK;
 }
@@ -413,6 +476,9 @@ extern "C" int gh_ctx_create(int device, gh_ctx** out) {
   for (uint32_t ml : {3u, 4u})
     for (uint32_t gv : {2u, 3u, 4u})
       (void)hipFuncSetAttribute(tile_kernel_for(ml, gv), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  for (int gl : {2, 3, 4})
+    for (int ns : {4, 6, 8})
+      (void)hipFuncSetAttribute(mtile_kernel_for(gl, ns), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   (void)hipGetLastError();
   *out = c;
   return GH_OK;
@@ -473,7 +539,8 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
     // width below maxlen leaves the code to the wave split).
     const char* envm = getenv("GH_MODE");
     const bool force_tile = envm && !strcmp(envm, "tile"), force_ws = envm && !strcmp(envm, "wsplit");
-    if (envm && *envm && !force_tile && !force_ws) return fail(GH_E_ARG, "GH_MODE: tile or wsplit");
+    const bool force_mt = envm && !strcmp(envm, "mtile");
+    if (envm && *envm && !force_tile && !force_ws && !force_mt) return fail(GH_E_ARG, "GH_MODE: tile, mtile or wsplit");
     const char* envk = getenv("GH_LUT_BITS");
     const uint32_t K = envk ? (uint32_t)std::clamp(atoi(envk), 1, 12) : cn.maxlen;
     const bool grouped = (grouped_code(cn) || short_code(cn)) && K >= cn.maxlen;
@@ -483,6 +550,19 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
     if (grouped && !force_ws) {
       if ((rc = tile_setup(c, K, avg))) return rc;
       if (force_tile && !c->tile) return fail(GH_E_HIP, "GH_MODE=tile: the tile kernel does not fit a CU");
+    }
+    // the two-pass tile kernel: codes of 2..12-bit codewords the single-pass one does not
+    // take (GH_MTILE=1; GH_MODE=mtile forces it)
+    const bool multi = cn.minlen >= 2 && cn.maxlen <= 12 && kraft16(cn) == 65536;
+    if (force_mt && !multi)
+      return fail(GH_E_ARG, "GH_MODE=mtile: the code is not for the two-pass tile kernel (complete, 2..12 bits)");
+    static const bool mt_on = [] {
+      const char* e = getenv("GH_MTILE");
+      return e && e[0] == '1';
+    }();
+    if (!c->tile && multi && (force_mt || (mt_on && !force_ws && !force_tile))) {
+      if ((rc = mtile_setup(c, avg))) return rc;
+      if (force_mt && !c->tile) return fail(GH_E_HIP, "GH_MODE=mtile: the two-pass tile kernel does not fit a CU");
     }
     if (!c->tile && (rc = ws_setup(c, avg))) return rc;
   }
@@ -723,12 +803,12 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     t.stamps = c->d_stamps;
     t.tstamps = c->d_stamps ? (unsigned long long*)((uint8_t*)c->d_stamps + 32ull * c->grid * 2 * 128) : nullptr;
     t.idle_block = c->idle_block;
-    const void* kern = tile_kernel_for(c->tile_minl, c->tile_g);
+    const void* kern = c->mtile ? mtile_kernel_for(c->mt_gl, c->mt_ns) : tile_kernel_for(c->tile_minl, c->tile_g);
     static thread_local void* ta[1];
     static thread_local TileParams tp;
     tp = t;
     ta[0] = &tp;
-    GH_HIP(hipLaunchKernel(kern, dim3(c->grid), dim3(TILE_TB), ta, c->lds, st));
+    GH_HIP(hipLaunchKernel(kern, dim3(c->grid), dim3(c->mtile ? MT_TB : TILE_TB), ta, c->lds, st));
     GH_HIP(hipEventRecord(dc.last, st));
     dc.has = true;
   }
@@ -785,9 +865,9 @@ extern "C" int gh_ctx_report(gh_ctx* c, void* hip_stream, gh_report* rep) {
     rep->lut_bits = c->tile ? c->tile_k : c->ws_k;
     rep->grid = c->grid;
     rep->tiles = c->ntiles;
-    rep->mode = c->tile ? GH_MODE_TILE : GH_MODE_SPLIT;
+    rep->mode = c->mtile ? GH_MODE_MTILE : c->tile ? GH_MODE_TILE : GH_MODE_SPLIT;
     std::memcpy(&rep->slow_lookbacks, misc + 4, 8);
-    rep->path = c->tile ? GH_PATH_GROUPED : GH_PATH_MULTI_WAVE;
+    rep->path = c->mtile ? GH_PATH_MULTI_TILE : c->tile ? GH_PATH_GROUPED : GH_PATH_MULTI_WAVE;
     rep->launches = c->nlaunch;
     rep->kernel_ms = c->nlaunch ? (float)(c->acc_ms / c->nlaunch) : 0.f;
   }

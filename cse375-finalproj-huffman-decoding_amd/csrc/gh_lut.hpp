@@ -111,6 +111,20 @@ inline std::vector<uint64_t> write_lut(const Canon& c, uint32_t K) {
   return t;
 }
 
+// Two-pass tile kernel LUT (gh_mtile.hip): entry i = {symbols, b | n << 8 | startmask << 16},
+// the write LUT's up to four codewords plus their starts (bit s: a codeword starts at
+// window bit s; bit 0 whenever n > 0).
+inline std::vector<uint64_t> multi_lut(const Canon& c, uint32_t K) {
+  std::vector<uint64_t> t(1u << K);
+  for (uint32_t i = 0; i < (1u << K); ++i) {
+    uint32_t n = 0, s = 0, m = 0;
+    const uint32_t b = window_codewords(c, i, K, 4, &n, &s, &m);
+    const uint32_t starts = n ? (1u | (m << 1)) & ((1u << b) - 1u) : 0u;
+    t[i] = (uint64_t)s | ((uint64_t)(b | (n << 8) | (starts << 16)) << 32);
+  }
+  return t;
+}
+
 // Wave-split count LUT: entry i = b | end mask << 16, every codeword of the window
 // (Kc <= 14, so the mask fits 16 bits).  Returns the expected bits per lookup on random
 // input bits (*out may be null: the estimate only).

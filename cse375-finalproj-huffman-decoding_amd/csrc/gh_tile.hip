@@ -448,8 +448,9 @@ __device__ __forceinline__ void copy_out_piece(uint8_t* out, uint32_t stg, unsig
   else if (t < nh + nt) k = 16u * ce + (t - nh);
   uint32_t b;
   asm volatile("ds_read_u8 %0, %1" : "=v"(b) : "v"(src + (k == OOB_OFF ? 0u : k)) : "memory");
-  if constexpr (NS == 4) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(b)::"memory");
-  else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(b)::"memory");
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b)::"memory");
+#pragma unroll
+  for (int i = 0; i < NS; ++i) asm volatile("" : "+v"(v[i]));  // (after the wait: asm volatile order)
 #pragma unroll
   for (int i = 0; i < NS; ++i) __builtin_amdgcn_raw_buffer_store_b128(v[i], rs, (int)off[i], 0, 2);  // nt
   __builtin_amdgcn_raw_buffer_store_b8((uint8_t)b, rs, (int)k, 0, 2);

@@ -105,8 +105,8 @@ class gh_sync_report(ctypes.Structure):
                 ("kernel_ms", ctypes.c_float)]
 
 
-MODE_NAMES = {1: "split", 2: "tile", 3: "fused"}
-PATH_NAMES = {2: "grouped", 4: "multi_wave"}
+MODE_NAMES = {1: "split", 2: "tile", 3: "fused", 4: "mtile"}
+PATH_NAMES = {2: "grouped", 4: "multi_wave", 8: "multi_tile"}
 
 
 class gh_opts(ctypes.Structure):

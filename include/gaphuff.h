@@ -148,7 +148,7 @@ typedef struct gh_report {
   uint32_t tiles;          /* segment tiles in the shard                            */
   float kernel_ms;         /* average time of one decode (all its kernels), events  */
   uint32_t launches;       /* decodes averaged in kernel_ms                         */
-  uint32_t mode;           /* GH_MODE_SPLIT or GH_MODE_TILE                         */
+  uint32_t mode;           /* GH_MODE_SPLIT, GH_MODE_TILE or GH_MODE_MTILE          */
   uint32_t path;           /* GH_PATH_*: table / decode-loop variant                */
   uint64_t slow_lookbacks; /* tile mode: prefix reads that had to poll              */
 } gh_report;
@@ -156,9 +156,12 @@ typedef struct gh_report {
 #define GH_MODE_SPLIT 1u    /* wave split: count, scan and write kernels (gh_wsplit.hip) */
 #define GH_MODE_TILE 2u     /* persistent tile kernel, round-leader prefixes (gh_tile.hip) */
 #define GH_MODE_FUSED 3u    /* reserved: the fused count + write tile kernel (removed)    */
+#define GH_MODE_MTILE 4u    /* two-pass tile kernel: count and write over register-resident
+                               words, one payload read (gh_mtile.hip) */
 #define GH_PATH_GROUPED 2u  /* one codeword per lookup, grouped window shifts (tile kernel) */
 #define GH_PATH_MULTI_WAVE 4u /* up to four codewords per lookup, canonical fallback for
                                  longer or incomplete codes (wave split) */
+#define GH_PATH_MULTI_TILE 8u /* up to four codewords per lookup, start masks (two-pass tile) */
 /* (values 0, 1, 3 were retired structures; they are no longer reported) */
 
 #define GH_ST_BADCODE 1u    /* a bit pattern outside the code space was met       */
