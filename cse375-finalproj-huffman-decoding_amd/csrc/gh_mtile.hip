@@ -27,12 +27,12 @@
 //
 // Write overruns: a lookup's four bytes past its n symbols are zeros, and the lookup that
 // reaches a segment's end writes up to three bytes past it, over the next segment's first
-// three bytes, which that segment (another lane, in lock-step) wrote earlier.  The bytes
-// up to the lookup's n symbols are the next segment's own first symbols (the stream goes
-// on at the gap-array start), but the zeros after them are not.  So every segment keeps
-// its first three bytes in a register (from its first three lookups) and stores them again
-// after the wave's last lookup (a wave's LDS operations complete in order).  A segment
-// has at least floor(113 / 12) = 9 codewords, so these head stores never overlap.
+// bytes, which that segment (another lane, in lock-step) wrote earlier; a finished
+// segment's lane goes on writing (no branch) at its end, i.e. over the next segment's
+// first four bytes.  So every segment keeps its first four bytes in a register (from its
+// first four lookups: each holds at least one codeword) and stores them again after the
+// wave's last lookup (a wave's LDS operations complete in order).  A segment has at least
+// floor(113 / 12) = 9 codewords, so these head stores never overlap.
 //
 // The prefix of tile k-1 is needed one iteration after its aggregate left (the count
 // pass is the first thing an iteration does, the prefix wait the last), with one staging
@@ -124,7 +124,7 @@ __device__ __forceinline__ void mt_write(uint32_t (&e)[U][5], const uint32_t (&o
     head[u] = 0;
   }
   auto group = [&](auto first) {
-    constexpr int L0 = decltype(first)::value;  // index of the group's first lookup (< 3: head bytes), or 3
+    constexpr int L0 = decltype(first)::value;  // index of the group's first lookup (< 4: head bytes), or 4
     uint32_t q[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) q[u] = 32u;
@@ -139,12 +139,14 @@ __device__ __forceinline__ void mt_write(uint32_t (&e)[U][5], const uint32_t (&o
       lds_wait(ent);
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        if (ptr[u] < end[u]) lds_st32(ptr[u], ent[u].x);  // unaligned: gfx950 LDS runs in unaligned mode
+        // unaligned (gfx950 LDS runs in unaligned mode); a finished segment keeps
+        // writing at its end, over the next segment's head (restored below)
+        lds_st32(min(ptr[u], end[u]), ent[u].x);
         if (L0 + j == 0) {  // (constants once unrolled)
           head[u] = ent[u].x;
-        } else if (L0 + j < 3) {
+        } else if (L0 + j < 4) {
           const uint32_t pos = ptr[u] - o[u];  // bytes so far (>= L0 + j)
-          head[u] = pos < 3u ? head[u] | (ent[u].x << (8u * pos)) : head[u];
+          head[u] = pos < 4u ? head[u] | (ent[u].x << (8u * pos)) : head[u];
         }
         ptr[u] = add_n(ptr[u], ent[u].y);
         q[u] -= ent[u].y;
@@ -160,16 +162,17 @@ __device__ __forceinline__ void mt_write(uint32_t (&e)[U][5], const uint32_t (&o
   };
   // the first groups carry the head bytes (static lookup indices), the rest loop
   bool more = group(std::integral_constant<int, 0>{});
-  if (GL < 3) more = group(std::integral_constant<int, GL>{}) || more;  // lookups 2.. (GL = 2)
+  if (GL < 4) more = group(std::integral_constant<int, GL>{}) || more;  // lookups GL.. 2GL-1 >= 3
   if (__any(more)) {
     for (int g = 0; g < MT_GMAX; ++g) {
-      if (!__any(group(std::integral_constant<int, 3>{}))) break;
+      if (!__any(group(std::integral_constant<int, 4>{}))) break;
     }
   }
   // every lane's lookups are done: the head bytes over the previous segment's overrun
+  // and end writes (in wave order: after them)
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    if (n[u]) asm volatile("ds_write_b16 %0, %1\n\tds_write_b8_d16_hi %0, %1 offset:2" ::"v"(o[u]), "v"(head[u]) : "memory");
+    if (n[u]) lds_st32(o[u], head[u]);
   }
 }
 
