@@ -547,7 +547,7 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
     if (force_tile && !grouped)
       return fail(GH_E_ARG, "GH_MODE=tile: the code is not for the tile kernel (complete, 3..12 bits)");
     const double avg = s->g ? (double)s->n / (double)s->g : 16.0;
-    if (grouped && !force_ws) {
+    if (grouped && !force_ws && !force_mt) {
       if ((rc = tile_setup(c, K, avg))) return rc;
       if (force_tile && !c->tile) return fail(GH_E_HIP, "GH_MODE=tile: the tile kernel does not fit a CU");
     }

@@ -11,10 +11,10 @@ reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 data = gh.generate(375, r, n); img = gh.encode(data); s = gh.parse(img)
 alg = 4 * s.w + 4 * ((s.g + 7) // 8) + s.n
 d = gh.Decoder(0); d.load(s)
-for _ in range(int(os.environ.get("QO_WARM", "3"))): d.decode(timed=False)
+for _ in range(int(os.environ.get('QO_WARM', '3'))): d.decode(timed=False)
 d.report(); d.reset_timing()
 for _ in range(reps): d.decode()
 rep = d.report()
 ok = bool(np.array_equal(d.download(s.n), data)) and rep.status == 0
 print(f"{name} ms={rep.kernel_ms:.4f} frac={alg / rep.kernel_ms / 1e6 / 8000:.4f} mode={gh.MODE_NAMES.get(rep.mode)} "
-      f"K={rep.lut_bits} grid={rep.grid} st={rep.status} polls={rep.slow_lookbacks / (reps + int(os.environ.get("QO_WARM", "3"))):.0f} ok={ok}", flush=True)
+      f"K={rep.lut_bits} grid={rep.grid} st={rep.status} polls={rep.slow_lookbacks / (reps + int(os.environ.get('QO_WARM', '3'))):.0f} ok={ok}", flush=True)
