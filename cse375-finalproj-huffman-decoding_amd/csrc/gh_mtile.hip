@@ -45,6 +45,17 @@
 #endif
 constexpr int MT_TB = GH_MTILE_TB;  // threads per workgroup
 constexpr int MT_U = 2;             // segments per lane
+#ifndef GH_MT_ABLATE
+#define GH_MT_ABLATE 0  // diagnostic builds only, bits: 1 no count pass (40 symbols per segment),
+                        // 2 no write pass, 4 no prefix wait (fake offsets); output wrong
+#endif
+#ifndef GH_MT_WOR
+#define GH_MT_WOR 1  // write pass: 1 ORs into zeroed staging (two aligned ds_or_b32 per lookup,
+                     // the copy-out re-zeroes), 0 unaligned ds_write_b32 + head restore
+#endif
+#ifndef GH_MT_NOFB
+#define GH_MT_NOFB 0  // experiment: no chain-by-chain path
+#endif
 constexpr int MT_GMAX = 80;         // lookup groups per segment, at most (>= 2 bits per lookup)
 
 // Advance a 5-word e-window by 32 - (q & 31) bits.
@@ -139,10 +150,21 @@ __device__ __forceinline__ void mt_write(uint32_t (&e)[U][5], const uint32_t (&o
       lds_wait(ent);
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        // unaligned (gfx950 LDS runs in unaligned mode); a finished segment keeps
-        // writing at its end, over the next segment's head (restored below)
-        lds_st32(min(ptr[u], end[u]), ent[u].x);
-        if (L0 + j == 0) {  // (constants once unrolled)
+        if (GH_MT_WOR) {
+          // OR the four bytes into the two aligned dwords they span (zeroed staging; a
+          // finished segment ORs zero at its end)
+          const bool on = ptr[u] < end[u];
+          const uint32_t a = on ? ptr[u] : end[u];
+          const unsigned long long d = (unsigned long long)(on ? ent[u].x : 0u) << ((a & 3u) << 3);
+          asm volatile("ds_or_b32 %0, %1\n\tds_or_b32 %0, %2 offset:4" ::"v"(a & ~3u), "v"((uint32_t)d),
+                       "v"((uint32_t)(d >> 32)) : "memory");
+        } else {
+          // unaligned (gfx950 LDS runs in unaligned mode); a finished segment keeps
+          // writing at its end, over the next segment's head (restored below)
+          lds_st32(min(ptr[u], end[u]), ent[u].x);
+        }
+        if (GH_MT_WOR) {
+        } else if (L0 + j == 0) {  // (constants once unrolled)
           head[u] = ent[u].x;
         } else if (L0 + j < 4) {
           const uint32_t pos = ptr[u] - o[u];  // bytes so far (>= L0 + j)
@@ -172,8 +194,17 @@ __device__ __forceinline__ void mt_write(uint32_t (&e)[U][5], const uint32_t (&o
   // and end writes (in wave order: after them)
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    if (n[u]) lds_st32(o[u], head[u]);
+    if (!GH_MT_WOR && n[u]) lds_st32(o[u], head[u]);
   }
+}
+
+// Zero the staging a write pass ORed into: piece bytes [0, n) and the last lookups'
+// overrun (the last lookup ORs two dwords: < 8 bytes past), i.e. region chunks [1, ce).  LDS operations
+// of a wave complete in order: after the copy-out's reads.
+__device__ __forceinline__ void mt_zero(uint32_t region, uint32_t n, int lane) {
+  const uint32_t ce = (STAGE_PAD + n + 8u + 15u) >> 4;
+  for (uint32_t c = 1u + (uint32_t)lane; c < ce; c += 64u)
+    asm volatile("ds_write_b128 %0, %1" ::"v"(region + 16u * c), "v"(tile_v4u{0, 0, 0, 0}) : "memory");
 }
 
 template <int TB, int GL, int NS>
@@ -196,10 +227,11 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     tile_round_leader<TB>(p, D, s_lead, tid, lane, wid);
     return;
   }
-  {  // LUT to LDS (u64 entries, one copy)
+  {  // LUT to LDS (u64 entries, one copy); zeroed staging regions
     const uint4* g = (const uint4*)p.lut;
     uint4* s4 = (uint4*)smem;
     for (uint32_t i = tid; i < p.lut_bytes / 16; i += TB) s4[i] = g[i];
+    for (uint32_t i = tid; i < NW * p.stage_bytes / 16; i += TB) s4[p.lut_bytes / 16 + i] = make_uint4(0, 0, 0, 0);
     if (tid < TILE_SLOTS) {
       s_cnt[tid] = 0;
       s_ptile[tid] = 0xFFFFFFFFu;
@@ -222,7 +254,10 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t sc = min(seg0 + (uint32_t)(64 * u), nseg - 1);
-      w[u] = *(const uint4*)(p.payload + 4ull * sc);
+      // nontemporal: read once (and not merged with the look-ahead dword into an
+      // overlapping load, which left register copies and a vmcnt wait at the loop's back edge)
+      const tile_v4u v = __builtin_nontemporal_load((const tile_v4u*)(p.payload + 4ull * sc));
+      w[u] = make_uint4(v.x, v.y, v.z, v.w);
       w4[u] = p.payload[4ull * sc + 4];
       gw[u] = p.gaps[(p.gap_nib0 + (sc ? sc - 1u : 0u)) >> 3];
     }
@@ -231,7 +266,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
   {  // as many stores after these loads as every iteration issues after its prefetch
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(p.out, 0, 0x7FFFFFF0, 0x00020000);
 #pragma unroll
-    for (int i = 0; i < NS; ++i) __builtin_amdgcn_raw_buffer_store_b128(tile_v4u{0, 0, 0, 0}, rs, (int)OOB_OFF, 0, 2);
+    for (int i = 0; i < NS; ++i) __builtin_amdgcn_raw_buffer_store_b128(tile_v4u{0, 0, 0, 0}, rs, (int)(OOB_OFF + 16u * (uint32_t)i), 0, 2);  // (distinct: not merged)
     __builtin_amdgcn_raw_buffer_store_b8((uint8_t)0, rs, (int)OOB_OFF, 0, 2);
   }
   if (cur >= p.ntiles) cur = NONE;
@@ -246,6 +281,11 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     for (int i = 0; i < 5; ++i) he[u][i] = 0;
   }
   uint32_t rank = 0;
+  // the copy-out's data registers, carried from one copy-out to the next (gh_tile.hip)
+  tile_v4u cv[NS];
+  uint32_t cb = 0;
+#pragma unroll
+  for (int i = 0; i < NS; ++i) cv[i] = tile_v4u{0, 0, 0, 0};
   const uint32_t region = stage_lds + (uint32_t)wid * p.stage_bytes;
   const uint32_t piece_cap = p.stage_bytes - (uint32_t)(STAGE_PAD + 8);
   for (uint32_t k = 0;; ++k) {
@@ -279,7 +319,12 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
 #pragma unroll
         for (int i = 0; i < 5; ++i) ce[u][i] = e[u][i];
       }
-      mt_count<U, GL>(e, R, cnt, amask);
+      if (GH_MT_ABLATE & 1) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) cnt[u] = R[u] > 0 ? 40u : 0u;
+      } else {
+        mt_count<U, GL>(e, R, cnt, amask);
+      }
     }
     const unsigned long long gp = __hip_atomic_load(pf2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     load(nxt);
@@ -316,8 +361,8 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
       }
     }
     // ---- write pass of tile k-1 into the wave's region (local offsets: no prefix needed)
-    const bool fits = htot <= piece_cap;
-    if (have2 && fits) {
+    const bool fits = GH_MT_NOFB ? true : htot <= piece_cap;
+    if (have2 && fits && !(GH_MT_ABLATE & 2)) {
       uint32_t o[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) o[u] = region + STAGE_PAD + hpos[u];
@@ -327,7 +372,10 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     unsigned long long goff = 0;
     uint32_t n2 = 0;
     bool got = true;
-    if (have2) {
+    if (have2 && (GH_MT_ABLATE & 4)) {
+      goff = ((unsigned long long)t2 * (U * TB * 40) + (uint32_t)wid * (U * 64 * 40)) % (p.out_cap - (U * TB * 64));
+      n2 = (uint32_t)min<unsigned long long>(htot, p.out_cap - goff);
+    } else if (have2) {
       unsigned long long g = rfl_u64(gp0);
       if (!granule_ok(p, g, 2)) {
         g = rfl_u64(gp);
@@ -371,7 +419,8 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     }
     // ---- copy-out ---------------------------------------------------------------------------
     if (fits) {
-      copy_out_piece<NS>(p.out, region, goff, n2, lane);  // fixed store count (n2 = 0: all dropped)
+      copy_out_piece<NS>(p.out, region, goff, n2, lane, cv, cb);  // fixed store count (n2 = 0: all dropped)
+      if (GH_MT_WOR) mt_zero(region, htot, lane);
     } else {
       // a piece larger than the region (data whose shortest codewords cluster): one chain
       // at a time (a chain's worst case fits), then drain (rare path)
@@ -382,7 +431,9 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
         uint32_t o[U], nn[U];
 #pragma unroll
         for (int v = 0; v < U; ++v) {
-          o[v] = region + STAGE_PAD + (hpos[v] - c0);
+          // the other chains write nothing of theirs: their (branch-free) stores go to
+          // the region's pad, before piece byte 0
+          o[v] = v == u ? region + STAGE_PAD + (hpos[v] - c0) : region;
           nn[v] = v == u ? hcnt[v] : 0u;
         }
         uint32_t ew[U][5];
@@ -393,7 +444,8 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
         mt_write<U, GL>(ew, o, nn, amask);
         const unsigned long long gu = goff + c0;
         const uint32_t nu = (!got || gu >= p.out_cap) ? 0u : (uint32_t)min<unsigned long long>(ct, p.out_cap - gu);
-        copy_out_piece<NS>(p.out, region, gu, nu, lane);
+        copy_out_piece<NS>(p.out, region, gu, nu, lane, cv, cb);
+        if (GH_MT_WOR) mt_zero(region, ct, lane);
       }
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     }

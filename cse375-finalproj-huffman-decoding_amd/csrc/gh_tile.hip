@@ -421,21 +421,31 @@ __device__ __forceinline__ void stage_wave(const uint32_t (&ow)[U][OW], const ui
 // counted vmcnt instead of vmcnt(0), so a wave never waits for its copy-out's stores to
 // be acknowledged.  The host sizes the regions so that NS * 64 chunks cover a piece.
 constexpr uint32_t OOB_OFF = 0x80000000u;  // a buffer offset past every range: the store is dropped
-template <int NS>
+// v, b: the data registers.  A caller that keeps them alive across its loop (as values
+// carried from one copy-out to the next, "+v" below) keeps the register allocator from
+// handing them to other values while the stores are in flight: the compiler waits for
+// an outstanding store before its data registers are overwritten (vmcnt), so a reuse
+// right after the copy-out stalled the next iteration on the stores.
+template <int NS, bool PIN = true>
 __device__ __forceinline__ void copy_out_piece(uint8_t* out, uint32_t stg, unsigned long long goff, uint32_t n,
-                                               int lane) {
+                                               int lane, tile_v4u (&v)[NS], uint32_t& b) {
+  // goff and n are wave-uniform; said so explicitly, the buffer resource lives in SGPRs
+  // (otherwise each store became a readfirstlane "waterfall" loop, and the compiler's
+  // vmcnt counting across those loops fell back to short counts at the next iteration)
+  goff = rfl_u64(goff);
+  n = (uint32_t)__builtin_amdgcn_readfirstlane((int)n);
   const uint32_t lb = (uint32_t)(goff & 15);
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out + (goff - lb), 0, 0x7FFFFFF0, 0x00020000);
   const uint32_t src = stg + 16u - lb;    // staging address of output chunk 0
   const uint32_t cf = lb ? 1u : 0u;       // interior chunks [cf, ce)
   const uint32_t ce = n ? (lb + n) >> 4 : 0u;
-  tile_v4u v[NS];
   uint32_t off[NS];
 #pragma unroll
   for (int i = 0; i < NS; ++i) {
     const uint32_t c = cf + (uint32_t)lane + 64u * (uint32_t)i;
     off[i] = c < ce ? 16u * c : OOB_OFF;
-    asm volatile("ds_read_b128 %0, %1" : "=v"(v[i]) : "v"(src + 16u * (c < ce ? c : cf)) : "memory");
+    if (PIN) asm volatile("ds_read_b128 %0, %1" : "+v"(v[i]) : "v"(src + 16u * (c < ce ? c : cf)) : "memory");
+    else asm volatile("ds_read_b128 %0, %1" : "=v"(v[i]) : "v"(src + 16u * (c < ce ? c : cf)) : "memory");
   }
   // edge bytes: the head chunk's [lb, min(16, lb + n)) when lb != 0, then the tail
   // chunk's [0, (lb + n) & 15) when it is another chunk; one byte per lane
@@ -446,8 +456,8 @@ __device__ __forceinline__ void copy_out_piece(uint8_t* out, uint32_t stg, unsig
   uint32_t k = OOB_OFF;
   if (t < nh) k = lb + t;
   else if (t < nh + nt) k = 16u * ce + (t - nh);
-  uint32_t b;
-  asm volatile("ds_read_u8 %0, %1" : "=v"(b) : "v"(src + (k == OOB_OFF ? 0u : k)) : "memory");
+  if (PIN) asm volatile("ds_read_u8 %0, %1" : "+v"(b) : "v"(src + (k == OOB_OFF ? 0u : k)) : "memory");
+  else asm volatile("ds_read_u8 %0, %1" : "=v"(b) : "v"(src + (k == OOB_OFF ? 0u : k)) : "memory");
   asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b)::"memory");
 #pragma unroll
   for (int i = 0; i < NS; ++i) asm volatile("" : "+v"(v[i]));  // (after the wait: asm volatile order)
@@ -648,7 +658,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(p.out, 0, 0x7FFFFFF0, 0x00020000);
 #pragma unroll
     for (int i = 0; i < TILE_NS; ++i)
-      __builtin_amdgcn_raw_buffer_store_b128(tile_v4u{0, 0, 0, 0}, rs, (int)OOB_OFF, 0, 2);
+      __builtin_amdgcn_raw_buffer_store_b128(tile_v4u{0, 0, 0, 0}, rs, (int)(OOB_OFF + 16u * (uint32_t)i), 0, 2);  // (distinct: not merged)
     __builtin_amdgcn_raw_buffer_store_b8((uint8_t)0, rs, (int)OOB_OFF, 0, 2);
   }
   if (cur >= p.ntiles) cur = NONE;
@@ -850,7 +860,11 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     // Unconditional (nothing to copy: n2 = 0, every store dropped): the same store count
     // on every path lets the compiler wait for the prefetched loads with a counted vmcnt
     // at the top of the next iteration.
-    if (!(GH_TILE_ABLATE & 8)) copy_out_piece<TILE_NS>(p.out, region0 + buf * NW * p.stage_bytes, goff, n2, lane);
+    if (!(GH_TILE_ABLATE & 8)) {
+      tile_v4u cv[TILE_NS];
+      uint32_t cb;
+      copy_out_piece<TILE_NS, false>(p.out, region0 + buf * NW * p.stage_bytes, goff, n2, lane, cv, cb);
+    }
     TSTAMP(5);
     // ---- stage this tile's piece (copied out LAG iterations later) ----------------------
     // a piece larger than the region (data whose shortest codewords cluster) waits for
