@@ -57,7 +57,14 @@ using namespace gh;
 // per segment, e.g. BASELINE's r = 0.5 codes) two segments per lane with 11 words (the
 // registers and the staging of a third segment would halve the workgroups per CU).
 static uint32_t tile_u_for(uint32_t minlen) { return minlen >= 4 ? (uint32_t)TILE_U : (uint32_t)TILE_U3; }
+#ifndef GH_TILE_OW7
+#define GH_TILE_OW7 1  // codes of >= 5-bit codewords: 7 output words per segment (<= 26 codewords)
+#endif
 static const void* tile_kernel_for(uint32_t minlen, uint32_t g) {
+  if (minlen >= 5 && GH_TILE_OW7)
+    return g >= 4 ? (const void*)gh_tile_kernel<TILE_TB, TILE_U, 4, 7, 5>
+         : g == 3 ? (const void*)gh_tile_kernel<TILE_TB, TILE_U, 3, 7, 5>
+                  : (const void*)gh_tile_kernel<TILE_TB, TILE_U, 2, 7, 5>;
   if (minlen >= 4)
     return g >= 4 ? (const void*)gh_tile_kernel<TILE_TB, TILE_U, 4, 8, 4>
          : g == 3 ? (const void*)gh_tile_kernel<TILE_TB, TILE_U, 3, 8, 4>
@@ -191,7 +198,7 @@ static int tile_setup(gh_ctx* c, uint32_t K, double avg_seg_bytes) {
   const uint32_t maxsyms = (128 + cn.minlen - 1) / cn.minlen;  // <= 43 (minlen >= 3)
   c->tile_k = K;
   c->tile_g = std::min<uint32_t>(4, 32 / cn.maxlen);
-  c->tile_minl = cn.minlen >= 4 ? 4 : 3;
+  c->tile_minl = cn.minlen >= 5 && GH_TILE_OW7 ? 5 : cn.minlen >= 4 ? 4 : 3;
   c->tile_u = tile_u_for(cn.minlen);
   c->ntiles = (uint32_t)ceil_div(c->nseg, (uint64_t)c->tile_u * TILE_TB);
   // Staging is sized for the typical piece, not the worst case (128 / minlen bytes per
@@ -205,7 +212,7 @@ static int tile_setup(gh_ctx* c, uint32_t K, double avg_seg_bytes) {
   uint64_t per_seg = std::min<uint64_t>(
       maxsyms, cn.minlen >= 4 ? (uint64_t)TILE_SCAP : (uint64_t)std::ceil(std::max(avg_seg_bytes, 1.0) * scapf + 1));
   if (const char* e = getenv("GH_TILE_SCAP")) per_seg = std::min<uint64_t>(maxsyms, (uint64_t)std::max(1, atoi(e)));
-  const uint64_t margin = 4ull * (cn.minlen >= 4 ? 8 : 11) + 4;  // garbage past a piece's end (4 OW + 4)
+  const uint64_t margin = 4ull * (cn.minlen >= 4 ? 8 : 11) + 4;  // garbage past a piece's end (4 OW + 4, OW <= 8 / 11)
   const uint64_t seg_wave = 64ull * c->tile_u;
   per_seg = std::min<uint64_t>(per_seg, ((uint64_t)TILE_NS * 64 * 16 - 2 * STAGE_PAD - margin) / seg_wave);
   c->stage_bytes = (uint32_t)((STAGE_PAD + seg_wave * per_seg + margin + 15) & ~15ull);
@@ -473,7 +480,7 @@ extern "C" int gh_ctx_create(int device, gh_ctx** out) {
   GH_HIP(hipEventCreateWithFlags(&c->done, hipEventDisableTiming));
   GH_HIP(hipMalloc(&c->d_misc, 128));
   GH_HIP(hipMemset(c->d_misc, 0, 128));
-  for (uint32_t ml : {3u, 4u})
+  for (uint32_t ml : {3u, 4u, 5u})
     for (uint32_t gv : {2u, 3u, 4u})
       (void)hipFuncSetAttribute(tile_kernel_for(ml, gv), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   for (int gl : {2, 3, 4})

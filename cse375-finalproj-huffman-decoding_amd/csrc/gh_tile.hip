@@ -61,7 +61,7 @@ constexpr int TILE_SLOTS = 16;  // per-tile wave totals / offsets / arrival coun
 #define TSTAMP(i) ((void)0)
 #endif
 #ifndef GH_TILE_ROLL
-#define GH_TILE_ROLL 0  // the decode's chains rolling (decode_tile_rolling) instead of in lock-step
+#define GH_TILE_ROLL 1  // the decode's chains rolling (decode_tile_rolling) instead of in lock-step (round 5: cfg4 -0.7 %, cfg5 -2 %)
 #endif
 #ifndef GH_TILE_CBORROW
 #define GH_TILE_CBORROW 0  // the decode's borrow count in C instead of inline asm
@@ -71,6 +71,9 @@ constexpr int TILE_SLOTS = 16;  // per-tile wave totals / offsets / arrival coun
 #endif
 #ifndef GH_TILE_LATEPF
 #define GH_TILE_LATEPF 0  // the next tile's loads after the prefix check instead of right after the decode
+#endif
+#ifndef GH_TILE_TOUCH
+#define GH_TILE_TOUCH 0  // one load per thread into the cache lines of the tile after next (L2 warm-up)
 #endif
 #ifndef GH_TILE_ABLATE
 #define GH_TILE_ABLATE 0  // diagnostic builds only (make variant), bits: 1 no decode, 2 no staging
@@ -665,6 +668,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
   uint32_t th[TILE_LAG];          // this wave's pieces of iterations k-1 .. k-LAG (NONE: not staged)
 #pragma unroll
   for (int i = 0; i < TILE_LAG; ++i) th[i] = NONE;
+  uint32_t sink = 0;              // (GH_TILE_TOUCH) the touch load's value, never used
   bool ahead = false;             // the last prefix had to be polled
   uint32_t rank = 0;              // (GH_TILE_RANKPRIO) the wave's arrival rank at its last tile, in quarters
   const uint32_t region0 = stage_lds + (uint32_t)wid * p.stage_bytes;  // buffer 0; buffer 1 at + NW * stage_bytes
@@ -751,7 +755,19 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     // copy-out instead they had ~3 K cycles, and the next decode waited ~1.3 K cycles for
     // them.  They follow the prefix loads, whose waits therefore do not include them
     // (vmcnt is one in-order queue).
+    if (GH_TILE_TOUCH) asm volatile("" ::"v"(sink));  // the last touch (one iteration old)
     if (!GH_TILE_LATEPF) load(nxt);
+    if (GH_TILE_TOUCH) {
+      // the tile after next: one dword of each of its payload and gap-word cache lines
+      // (128 B), so that its loads, issued one iteration from now, find them in L2
+      constexpr uint32_t PL = (uint32_t)(U * TB * 16 / 128);
+      const uint32_t tt = min(nxt + G, p.ntiles - 1);
+      const uint32_t l = (uint32_t)tid % (PL + (uint32_t)(U * TB / 256) + 1u);
+      const uint32_t* a = l < PL ? p.payload + min(4ull * tt * (U * TB) + 32ull * l, 4ull * nseg)
+                                 : p.gaps + min((p.gap_nib0 + tt * (uint32_t)(U * TB)) / 8u + 32u * (l - PL),
+                                                (p.gap_nib0 + nseg - 1u) / 8u);
+      sink = *a;
+    }
     TSTAMP(2);
     // ---- wave scans: the segments' offsets in the wave's piece, the piece's length -------
     uint32_t bpos[U], wave_tot = 0;
