@@ -278,7 +278,8 @@ static int mtile_setup(gh_ctx* c, double avg_seg_bytes) {
   uint64_t per_seg = std::min<uint64_t>(maxsyms, (uint64_t)std::ceil(std::max(avg_seg_bytes, 1.0) * scapf + 1));
   if (const char* e = getenv("GH_TILE_SCAP")) per_seg = std::min<uint64_t>(maxsyms, (uint64_t)std::max(1, atoi(e)));
   // at most what the LDS (LUT + 16 regions + slots) and the copy-out's 8 x 64 chunks hold
-  const uint64_t lds_free = 160ull * 1024 - (8ull << K) - mtile_lds_bytes(0, 0);
+  const uint64_t lut_b = (GH_MT_CLUT ? 12ull : 8ull) << K;  // write table (+ count table)
+  const uint64_t lds_free = 160ull * 1024 - lut_b - mtile_lds_bytes(0, 0);
   const uint64_t region_max = std::min<uint64_t>(lds_free / (MT_TB / 64), 8 * 1024 + STAGE_PAD) & ~15ull;
   per_seg = std::min<uint64_t>(per_seg, (region_max - STAGE_PAD - 16) / (64ull * MT_U));
   const uint64_t cap = std::max<uint64_t>(64ull * MT_U * per_seg, 64ull * maxsyms);  // piece bytes staged at once
@@ -287,15 +288,25 @@ static int mtile_setup(gh_ctx* c, double avg_seg_bytes) {
   c->stage_bytes = (uint32_t)((STAGE_PAD + cap + 16 + 15) & ~15ull);  // + the write overrun
   c->mt_gl = lookups_per_shift(K);
   const void* kern = mtile_kernel_for(c->mt_gl, c->mt_ns);
-  c->lut_bytes = 8ull << K;
+  c->lut_bytes = lut_b;
   c->lds = mtile_lds_bytes(c->lut_bytes, c->stage_bytes);
   int pc = 0;
   GH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, kern, MT_TB, c->lds));
   pc = std::min(pc, 2);  // (as tile_setup: the occupancy query can answer one too many)
   if (pc < 1) return GH_OK;
-  const std::vector<uint64_t> lt = multi_lut(cn, K);
-  GH_HIP(hipMalloc(&c->d_lut_t, 8ull << K));
-  GH_HIP(hipMemcpy(c->d_lut_t, lt.data(), 8ull << K, hipMemcpyHostToDevice));
+  std::vector<uint64_t> lt = multi_lut(cn, K);
+  if (GH_MT_CLUT) {  // the count table (u32 {b | start mask << 16}, every codeword of the window) after it
+    std::vector<uint32_t> lc(1u << K);
+    for (uint32_t i = 0; i < (1u << K); ++i) {
+      uint32_t n = 0, m = 0;
+      const uint32_t b = window_codewords(cn, i, K, 32, &n, nullptr, &m);
+      lc[i] = b | ((n ? (1u | (m << 1)) & ((1u << b) - 1u) : 0u) << 16);
+    }
+    lt.resize((12ull << K) / 8);
+    std::memcpy(lt.data() + (1u << K), lc.data(), 4ull << K);
+  }
+  GH_HIP(hipMalloc(&c->d_lut_t, lut_b));
+  GH_HIP(hipMemcpy(c->d_lut_t, lt.data(), lut_b, hipMemcpyHostToDevice));
   c->tile_k = K;
   c->lgr = 0;
   c->tile_u = MT_U;
@@ -699,6 +710,7 @@ struct DevChain {
   std::mutex mu;
   hipEvent_t last = nullptr;
   bool has = false;
+  hipStream_t last_stream = nullptr;  // the stream the last tile kernel ran on
 };
 static DevChain& dev_chain(int device) {
   static std::mutex mu;
@@ -731,7 +743,9 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     }
     chain_lock.lock();
     if (!dc.last) GH_HIP(hipEventCreateWithFlags(&dc.last, hipEventDisableTiming));
-    if (dc.has) GH_HIP(hipStreamWaitEvent(st, dc.last, 0));
+    // (a decode on the same stream as the last one is ordered behind it already: no wait
+    // packet, which cost the back-to-back cfg2 decodes ~10 us each)
+    if (dc.has && dc.last_stream != st) GH_HIP(hipStreamWaitEvent(st, dc.last, 0));
   }
   std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
   if (timed) {
@@ -818,6 +832,7 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     GH_HIP(hipLaunchKernel(kern, dim3(c->grid), dim3(c->mtile ? MT_TB : TILE_TB), ta, c->lds, st));
     GH_HIP(hipEventRecord(dc.last, st));
     dc.has = true;
+    dc.last_stream = st;
   }
   GH_HIP(hipGetLastError());
   if (timed) {

@@ -49,9 +49,19 @@ constexpr int MT_U = 2;             // segments per lane
 #define GH_MT_ABLATE 0  // diagnostic builds only, bits: 1 no count pass (40 symbols per segment),
                         // 2 no write pass, 4 no prefix wait (fake offsets); output wrong
 #endif
+#ifndef GH_MT_LAG
+#define GH_MT_LAG 2  // a tile is written and copied out LAG iterations after its count pass
+#endif
+constexpr int MT_LAG = GH_MT_LAG;
+#ifndef GH_MT_CLUT
+#define GH_MT_CLUT 1  // the count pass reads its own u32 table (all codewords of the window,
+                      // 4 << K bytes after the write table) instead of the write table's high words
+#endif
 #ifndef GH_MT_WOR
 #define GH_MT_WOR 1  // write pass: 1 ORs into zeroed staging (two aligned ds_or_b32 per lookup,
-                     // the copy-out re-zeroes), 0 unaligned ds_write_b32 + head restore
+                     // the copy-out re-zeroes), 2 the same with the bytes gathered into
+                     // aligned dwords first (one ds_or_b32 per lookup), 0 unaligned
+                     // ds_write_b32 + head restore
 #endif
 #ifndef GH_MT_NOFB
 #define GH_MT_NOFB 0  // experiment: no chain-by-chain path
@@ -78,7 +88,8 @@ inline size_t mtile_lds_bytes(size_t lut_bytes, size_t stage_bytes) {
 // that start before the segment end, R = 128 - start bits away.  GL lookups per window
 // shift (GL * K <= 24 bits: rm, recomputed per group from R, covers the group's starts).
 template <int U, int GL>
-__device__ __forceinline__ void mt_count(uint32_t (&e)[U][5], const int (&R0)[U], uint32_t (&cnt)[U], uint32_t amask) {
+__device__ __forceinline__ void mt_count(uint32_t (&e)[U][5], const int (&R0)[U], uint32_t (&cnt)[U], uint32_t amask,
+                                         uint32_t cbase) {
   int R[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
@@ -98,7 +109,7 @@ __device__ __forceinline__ void mt_count(uint32_t (&e)[U][5], const int (&R0)[U]
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const uint32_t x = j == 0 ? e[u][0] : __builtin_amdgcn_alignbit(e[u][0], e[u][1], q[u]);
-        hi[u] = lds_u32_nowait((x & amask) | 4u);  // the entry's high word
+        hi[u] = lds_u32_nowait((x & amask) | cbase);  // the count entry (or the write entry's high word)
       }
       lds_wait(hi);
 #pragma unroll
@@ -128,11 +139,18 @@ template <int U, int GL>
 __device__ __forceinline__ void mt_write(uint32_t (&e)[U][5], const uint32_t (&o)[U], const uint32_t (&n)[U],
                                          uint32_t amask) {
   uint32_t ptr[U], end[U], head[U];
+  uint32_t alo[U], ahi[U], fill[U], dptr[U];  // (GH_MT_WOR 2) pending bytes, their count, dword address
+  int rem[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     ptr[u] = o[u];
     end[u] = o[u] + n[u];
     head[u] = 0;
+    alo[u] = 0;
+    ahi[u] = 0;
+    fill[u] = o[u] & 3u;
+    dptr[u] = o[u] & ~3u;
+    rem[u] = (int)n[u];
   }
   auto group = [&](auto first) {
     constexpr int L0 = decltype(first)::value;  // index of the group's first lookup (< 4: head bytes), or 4
@@ -150,7 +168,24 @@ __device__ __forceinline__ void mt_write(uint32_t (&e)[U][5], const uint32_t (&o
       lds_wait(ent);
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        if (GH_MT_WOR) {
+        if (GH_MT_WOR == 2) {
+          // gather into the pending dword (bytes [fill, fill + n)), OR it at its aligned
+          // address (again as it fills up: ORing the same bytes twice is harmless), move on
+          // once it is complete; a finished segment ORs zero
+          const bool on = rem[u] > 0;
+          const unsigned long long d = (unsigned long long)(on ? ent[u].x : 0u) << (fill[u] << 3);
+          alo[u] |= (uint32_t)d;
+          ahi[u] |= (uint32_t)(d >> 32);
+          asm volatile("ds_or_b32 %0, %1" ::"v"(dptr[u]), "v"(alo[u]) : "memory");
+          const uint32_t nn = on ? __builtin_amdgcn_ubfe(ent[u].y, 8, 3) : 0u;
+          rem[u] -= (int)nn;
+          fill[u] += nn;
+          const bool adv = fill[u] >= 4u;
+          dptr[u] += adv ? 4u : 0u;
+          alo[u] = adv ? ahi[u] : alo[u];
+          ahi[u] = adv ? 0u : ahi[u];
+          fill[u] -= adv ? 4u : 0u;
+        } else if (GH_MT_WOR) {
           // OR the four bytes into the two aligned dwords they span (zeroed staging; a
           // finished segment ORs zero at its end)
           const bool on = ptr[u] < end[u];
@@ -178,7 +213,7 @@ __device__ __forceinline__ void mt_write(uint32_t (&e)[U][5], const uint32_t (&o
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       win_shift5(e[u], q[u]);
-      more |= ptr[u] < end[u];
+      more |= GH_MT_WOR == 2 ? rem[u] > 0 : ptr[u] < end[u];
     }
     return more;
   };
@@ -237,8 +272,13 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
       s_ptile[tid] = 0xFFFFFFFFu;
     }
   }
-  const uint32_t S = 29u - p.kbits;
+  const uint32_t S = 29u - p.kbits;                        // write pass: u64 entries
   const uint32_t amask = ((1u << p.kbits) - 1u) << 3;
+  // count pass: its own u32 table after the write table (GH_MT_CLUT), or the write
+  // table's high words
+  const uint32_t Sc = GH_MT_CLUT ? 30u - p.kbits : S;
+  const uint32_t amask_c = GH_MT_CLUT ? ((1u << p.kbits) - 1u) << 2 : amask;
+  const uint32_t cbase = GH_MT_CLUT ? 8u << p.kbits : 4u;
   check_lds_base(smem, p.status);
   const uint32_t G = D, b = blockIdx.x - 1;
   const uint32_t nseg = (uint32_t)p.nseg;
@@ -270,34 +310,38 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     __builtin_amdgcn_raw_buffer_store_b8((uint8_t)0, rs, (int)OOB_OFF, 0, 2);
   }
   if (cur >= p.ntiles) cur = NONE;
-  // tile k-1, held for its write pass: its e-windows, the segments' offsets in the
-  // wave's piece and counts, the piece's length
-  uint32_t th = NONE, he[U][5], hpos[U], hcnt[U], htot = 0;
+  // tiles k-1 .. k-LAG, held for their write pass: e-windows, the segments' offsets in
+  // the wave's piece and counts, the piece's length
+  constexpr int L = MT_LAG;
+  uint32_t th[L], he[L][U][5], hpos[L][U], hcnt[L][U], htot[L];
 #pragma unroll
-  for (int u = 0; u < U; ++u) {
-    hpos[u] = 0;
-    hcnt[u] = 0;
+  for (int i2 = 0; i2 < L; ++i2) {
+    th[i2] = NONE;
+    htot[i2] = 0;
 #pragma unroll
-    for (int i = 0; i < 5; ++i) he[u][i] = 0;
+    for (int u = 0; u < U; ++u) {
+      hpos[i2][u] = 0;
+      hcnt[i2][u] = 0;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) he[i2][u][i] = 0;
+    }
   }
   uint32_t rank = 0;
-  // the copy-out's data registers, carried from one copy-out to the next (gh_tile.hip)
-  tile_v4u cv[NS];
-  uint32_t cb = 0;
-#pragma unroll
-  for (int i = 0; i < NS; ++i) cv[i] = tile_v4u{0, 0, 0, 0};
   const uint32_t region = stage_lds + (uint32_t)wid * p.stage_bytes;
   const uint32_t piece_cap = p.stage_bytes - (uint32_t)(STAGE_PAD + 8);
   for (uint32_t k = 0;; ++k) {
     const bool have_cur = cur < p.ntiles;
-    const uint32_t t2 = th;  // the tile written and copied out this iteration
+    const uint32_t t2 = th[L - 1];  // the tile written and copied out this iteration
     const bool have2 = t2 < p.ntiles;
-    if (!have_cur && !have2) break;
-    if (last_tile_k != NONE && k > last_tile_k + 4) {  // cannot happen; never hang the GPU
+    bool pending = have_cur;
+#pragma unroll
+    for (int i2 = 0; i2 < L; ++i2) pending |= th[i2] < p.ntiles;
+    if (!pending) break;
+    if (last_tile_k != NONE && k > last_tile_k + L + 3) {  // cannot happen; never hang the GPU
       if (lane == 0) atomicOr(p.status, (unsigned)GH_ST_TIMEOUT);
       break;
     }
-    const uint32_t slot = k % TILE_SLOTS, slot2 = (k + TILE_SLOTS - 1) % TILE_SLOTS;
+    const uint32_t slot = k % TILE_SLOTS, slot2 = (k + TILE_SLOTS - L) % TILE_SLOTS;
     if (rank >= 3) __builtin_amdgcn_s_setprio(3);
     else if (rank == 2) __builtin_amdgcn_s_setprio(2);
     else if (rank == 1) __builtin_amdgcn_s_setprio(1);
@@ -315,15 +359,19 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
         const bool act = have_cur && seg < nseg;
         const int start = seg == 0 ? (int)p.first_start : (int)gap_nib(gw[u], p.gap_nib0 + seg - 1u);
         R[u] = act ? 128 - start : 0;
-        make_ewin(w[u], w4[u], start, S, e[u]);
+        make_ewin(w[u], w4[u], start, S, ce[u]);  // held for the write pass
+        if (GH_MT_CLUT) {
+          make_ewin(w[u], w4[u], start, Sc, e[u]);
+        } else {
 #pragma unroll
-        for (int i = 0; i < 5; ++i) ce[u][i] = e[u][i];
+          for (int i = 0; i < 5; ++i) e[u][i] = ce[u][i];
+        }
       }
       if (GH_MT_ABLATE & 1) {
 #pragma unroll
         for (int u = 0; u < U; ++u) cnt[u] = R[u] > 0 ? 40u : 0u;
       } else {
-        mt_count<U, GL>(e, R, cnt, amask);
+        mt_count<U, GL>(e, R, cnt, amask_c, cbase);
       }
     }
     const unsigned long long gp = __hip_atomic_load(pf2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -361,12 +409,13 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
       }
     }
     // ---- write pass of tile k-1 into the wave's region (local offsets: no prefix needed)
-    const bool fits = GH_MT_NOFB ? true : htot <= piece_cap;
+    const uint32_t wtot = htot[L - 1];
+    const bool fits = GH_MT_NOFB ? true : wtot <= piece_cap;
     if (have2 && fits && !(GH_MT_ABLATE & 2)) {
       uint32_t o[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) o[u] = region + STAGE_PAD + hpos[u];
-      mt_write<U, GL>(he, o, hcnt, amask);
+      for (int u = 0; u < U; ++u) o[u] = region + STAGE_PAD + hpos[L - 1][u];
+      mt_write<U, GL>(he[L - 1], o, hcnt[L - 1], amask);
     }
     // ---- the prefix of tile k-1 -> this wave's piece's output offset (gh_tile.hip) --------
     unsigned long long goff = 0;
@@ -374,7 +423,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     bool got = true;
     if (have2 && (GH_MT_ABLATE & 4)) {
       goff = ((unsigned long long)t2 * (U * TB * 40) + (uint32_t)wid * (U * 64 * 40)) % (p.out_cap - (U * TB * 64));
-      n2 = (uint32_t)min<unsigned long long>(htot, p.out_cap - goff);
+      n2 = (uint32_t)min<unsigned long long>(wtot, p.out_cap - goff);
     } else if (have2) {
       unsigned long long g = rfl_u64(gp0);
       if (!granule_ok(p, g, 2)) {
@@ -414,51 +463,68 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
       }
       asm volatile("" ::: "memory");
       goff = (g & GRAN_VMASK) + s_off[slot2 * NW + wid];
-      if (wid == NW - 1 && t2 == p.ntiles - 1 && got && lane == 0) *p.total = goff + htot;
-      n2 = (!got || goff >= p.out_cap) ? 0u : (uint32_t)min<unsigned long long>(htot, p.out_cap - goff);
+      if (wid == NW - 1 && t2 == p.ntiles - 1 && got && lane == 0) *p.total = goff + wtot;
+      n2 = (!got || goff >= p.out_cap) ? 0u : (uint32_t)min<unsigned long long>(wtot, p.out_cap - goff);
     }
     // ---- copy-out ---------------------------------------------------------------------------
     if (fits) {
-      copy_out_piece<NS>(p.out, region, goff, n2, lane, cv, cb);  // fixed store count (n2 = 0: all dropped)
-      if (GH_MT_WOR) mt_zero(region, htot, lane);
+      tile_v4u cv[NS];
+      uint32_t cb;
+      copy_out_piece<NS, false>(p.out, region, goff, n2, lane, cv, cb);  // fixed store count (n2 = 0: all dropped)
+      if (GH_MT_WOR) mt_zero(region, wtot, lane);
     } else {
       // a piece larger than the region (data whose shortest codewords cluster): one chain
       // at a time (a chain's worst case fits), then drain (rare path)
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const uint32_t c0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)hpos[u]);  // chain u's first byte
-        const uint32_t ct = (u + 1 < U ? (uint32_t)__builtin_amdgcn_readfirstlane((int)hpos[u + 1 < U ? u + 1 : u]) : htot) - c0;
+        const uint32_t c0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)hpos[L - 1][u]);  // chain u's first byte
+        const uint32_t ct = (u + 1 < U ? (uint32_t)__builtin_amdgcn_readfirstlane((int)hpos[L - 1][u + 1 < U ? u + 1 : u])
+                                       : wtot) - c0;
         uint32_t o[U], nn[U];
 #pragma unroll
         for (int v = 0; v < U; ++v) {
           // the other chains write nothing of theirs: their (branch-free) stores go to
           // the region's pad, before piece byte 0
-          o[v] = v == u ? region + STAGE_PAD + (hpos[v] - c0) : region;
-          nn[v] = v == u ? hcnt[v] : 0u;
+          o[v] = v == u ? region + STAGE_PAD + (hpos[L - 1][v] - c0) : region;
+          nn[v] = v == u ? hcnt[L - 1][v] : 0u;
         }
         uint32_t ew[U][5];
 #pragma unroll
         for (int v = 0; v < U; ++v)
 #pragma unroll
-          for (int i = 0; i < 5; ++i) ew[v][i] = he[v][i];
+          for (int i = 0; i < 5; ++i) ew[v][i] = he[L - 1][v][i];
         mt_write<U, GL>(ew, o, nn, amask);
         const unsigned long long gu = goff + c0;
         const uint32_t nu = (!got || gu >= p.out_cap) ? 0u : (uint32_t)min<unsigned long long>(ct, p.out_cap - gu);
-        copy_out_piece<NS>(p.out, region, gu, nu, lane, cv, cb);
+        tile_v4u cv[NS];
+        uint32_t cb;
+        copy_out_piece<NS, false>(p.out, region, gu, nu, lane, cv, cb);
         if (GH_MT_WOR) mt_zero(region, ct, lane);
       }
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     }
     // ---- hold tile k for its write pass -----------------------------------------------------
 #pragma unroll
+    for (int i2 = L - 1; i2 > 0; --i2) {
+      th[i2] = th[i2 - 1];
+      htot[i2] = htot[i2 - 1];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) he[i2][u][i] = he[i2 - 1][u][i];
+        hpos[i2][u] = hpos[i2 - 1][u];
+        hcnt[i2][u] = hcnt[i2 - 1][u];
+      }
+    }
+#pragma unroll
     for (int u = 0; u < U; ++u) {
 #pragma unroll
-      for (int i = 0; i < 5; ++i) he[u][i] = ce[u][i];
-      hpos[u] = bpos[u];
-      hcnt[u] = cnt[u];
+      for (int i = 0; i < 5; ++i) he[0][u][i] = ce[u][i];
+      hpos[0][u] = bpos[u];
+      hcnt[0][u] = cnt[u];
     }
-    htot = have_cur ? wave_tot : 0u;
-    th = have_cur ? cur : NONE;
+    htot[0] = have_cur ? wave_tot : 0u;
+    th[0] = have_cur ? cur : NONE;
     cur = nxt < p.ntiles ? nxt : NONE;
     nxt += G;
   }
