@@ -18,6 +18,7 @@
 // Every output write is clamped at the shard's output capacity (the reference wrote
 // past N, decoder.cu:672-728).  Tables: gh_lut.hpp; device helpers: gh_device.hpp.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <cmath>
@@ -116,6 +117,7 @@ struct gh_ctx {
   hipStream_t stream = nullptr;
   hipEvent_t done = nullptr;  // recorded after every decode, on the stream it ran on
   bool done_rec = false;
+  hipEvent_t done_ev = nullptr;    // marks the last decode: `done`, or the timed decode's end event
   bool loaded = false;
   Canon canon;
   // the loaded shard
@@ -508,10 +510,42 @@ extern "C" int gh_ctx_device(gh_ctx* c, int* device) {
   return GH_OK;
 }
 
+// The tile kernel's workgroups wait on each other (round prefixes): it assumes that the
+// whole grid becomes resident.  Two of them running at once on one device (several shard
+// contexts on one GPU, each on its own stream) can each hold half the CUs and wait
+// forever for the rest (their bounded spins then report GH_ST_TIMEOUT).  So launches
+// of such kernels on one device are chained: each waits for the previous one's
+// completion event, whatever stream either was launched on.
+struct DevChain {
+  std::mutex mu;
+  hipEvent_t last = nullptr;          // the last tile decode's done_ev (owned by `owner`)
+  const gh_ctx* owner = nullptr;
+  bool has = false;
+  hipStream_t last_stream = nullptr;  // the stream the last tile kernel ran on
+};
+static DevChain& dev_chain(int device) {
+  static std::mutex mu;
+  static std::map<int, DevChain*> m;
+  std::lock_guard<std::mutex> g(mu);
+  DevChain*& d = m[device];
+  if (!d) d = new DevChain();  // one per device, for the life of the process
+  return *d;
+}
+
 extern "C" int gh_ctx_destroy(gh_ctx* c) {
   if (!c) return GH_OK;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->done_rec) (void)hipEventSynchronize(c->done_ev);
+  {  // the device chain must not keep one of this context's events
+    DevChain& dc = dev_chain(c->device);
+    std::lock_guard<std::mutex> g(dc.mu);
+    if (dc.owner == c) {
+      dc.has = false;
+      dc.owner = nullptr;
+      dc.last = nullptr;
+    }
+  }
   free_shard(c);
   (void)hipFree(c->d_misc);
   for (auto& e : c->pending) {
@@ -700,27 +734,6 @@ extern "C" int gh_ctx_load_device(gh_ctx* c, const gh_stream* s, uint64_t b, uin
   return GH_OK;
 }
 
-// The tile kernel's workgroups wait on each other (round prefixes): it assumes that the
-// whole grid becomes resident.  Two of them running at once on one device (several shard
-// contexts on one GPU, each on its own stream) can each hold half the CUs and wait
-// forever for the rest (their bounded spins then report GH_ST_TIMEOUT).  So launches
-// of such kernels on one device are chained: each waits for the previous one's
-// completion event, whatever stream either was launched on.
-struct DevChain {
-  std::mutex mu;
-  hipEvent_t last = nullptr;
-  bool has = false;
-  hipStream_t last_stream = nullptr;  // the stream the last tile kernel ran on
-};
-static DevChain& dev_chain(int device) {
-  static std::mutex mu;
-  static std::map<int, DevChain*> m;
-  std::lock_guard<std::mutex> g(mu);
-  DevChain*& d = m[device];
-  if (!d) d = new DevChain();  // one per device, for the life of the process
-  return *d;
-}
-
 extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
   if (!c) return fail(GH_E_ARG, "null ctx");
   if (!c->loaded) return fail(GH_E_STATE, "gh_ctx_decode before gh_ctx_load");
@@ -729,6 +742,7 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
   if (c->nseg == 0) {
     GH_HIP(hipMemsetAsync(c->d_misc + 2, 0, 8, st));
     GH_HIP(hipEventRecord(c->done, st));
+    c->done_ev = c->done;
     c->done_rec = true;
     return GH_OK;
   }
@@ -742,9 +756,8 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
       c->epoch = 1;
     }
     chain_lock.lock();
-    if (!dc.last) GH_HIP(hipEventCreateWithFlags(&dc.last, hipEventDisableTiming));
     // (a decode on the same stream as the last one is ordered behind it already: no wait
-    // packet, which cost the back-to-back cfg2 decodes ~10 us each)
+    // packet)
     if (dc.has && dc.last_stream != st) GH_HIP(hipStreamWaitEvent(st, dc.last, 0));
   }
   std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
@@ -756,7 +769,7 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
       GH_HIP(hipEventCreate(&ev.first));
       GH_HIP(hipEventCreate(&ev.second));
     }
-    GH_HIP(hipEventRecord(ev.first, st));
+    if (!c->tile) GH_HIP(hipEventRecord(ev.first, st));  // (tile: in the dispatch itself, below)
   }
   if (c->ws) {
     WsParams m{};
@@ -829,25 +842,40 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     static thread_local TileParams tp;
     tp = t;
     ta[0] = &tp;
-    GH_HIP(hipLaunchKernel(kern, dim3(c->grid), dim3(c->mtile ? MT_TB : TILE_TB), ta, c->lds, st));
-    GH_HIP(hipEventRecord(dc.last, st));
+    // timed: the start and stop timestamps are taken by the dispatch packet itself
+    // (hipExtLaunchKernel), not by marker packets around it, so back-to-back decodes
+    // have no extra packets between them
+    if (timed)
+      GH_HIP(hipExtLaunchKernel(kern, dim3(c->grid), dim3(c->mtile ? MT_TB : TILE_TB), ta, c->lds, st, ev.first,
+                                ev.second, 0));
+    else
+      GH_HIP(hipLaunchKernel(kern, dim3(c->grid), dim3(c->mtile ? MT_TB : TILE_TB), ta, c->lds, st));
+  }
+  GH_HIP(hipGetLastError());
+  // one event after the kernel(s): the timed decode's end event, or `done` (each marker
+  // between back-to-back decodes costs the GPU microseconds)
+  if (timed) {
+    if (!c->tile) GH_HIP(hipEventRecord(ev.second, st));
+    c->pending.push_back(ev);
+    c->done_ev = ev.second;
+  } else {
+    GH_HIP(hipEventRecord(c->done, st));
+    c->done_ev = c->done;
+  }
+  c->done_rec = true;
+  if (c->tile) {  // the device chain's last decode (chain_lock held)
+    dc.last = c->done_ev;
+    dc.owner = c;
     dc.has = true;
     dc.last_stream = st;
   }
-  GH_HIP(hipGetLastError());
-  if (timed) {
-    GH_HIP(hipEventRecord(ev.second, st));
-    c->pending.push_back(ev);
-  }
-  GH_HIP(hipEventRecord(c->done, st));
-  c->done_rec = true;
   return GH_OK;
 }
 
 // Waits for the context's last decode, whatever stream it was launched on.
 static int wait_decode(gh_ctx* c) {
   GH_HIP(hipStreamSynchronize(c->stream));
-  if (c->done_rec) GH_HIP(hipEventSynchronize(c->done));
+  if (c->done_rec) GH_HIP(hipEventSynchronize(c->done_ev));
   return GH_OK;
 }
 
@@ -928,7 +956,7 @@ extern "C" int gh_ctx_copy_output(gh_ctx* c, uint64_t off, void* dst, uint64_t n
   if (!nbytes) return GH_OK;
   hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
   GH_HIP(hipSetDevice(c->device));
-  if (c->done_rec) GH_HIP(hipStreamWaitEvent(st, c->done, 0));  // after the last decode
+  if (c->done_rec) GH_HIP(hipStreamWaitEvent(st, c->done_ev, 0));  // after the last decode
   GH_HIP(hipMemcpyAsync(dst, c->d_out + off, nbytes, hipMemcpyDefault, st));
   return GH_OK;
 }

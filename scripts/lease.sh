@@ -14,7 +14,7 @@
 #   stats NAME WL             rocprofv3 --kernel-trace --stats of quick_one.py WL
 #   sq NAME WL [LIB]          two SQ counter passes (issue / wait / LDS) of quick_one.py WL
 #                             (LIB: a build variant's name, lib/libgaphuff_LIB.so)
-#   traffic NAME WL           FETCH_SIZE and WRITE_SIZE passes (separate runs)
+#   traffic NAME WL [V=x]     FETCH_SIZE and WRITE_SIZE passes (separate runs), with settings
 #   cmd NAME SECS CMD...      anything else, under its own time limit
 # WL: cfg2 | cfg3 | cfg4 | cfg5 | name:N:r.  Every step runs under its own `timeout -k`;
 # a fault / abort / time-limit kill (124, 134, 137, 139) ends the lease (gpu_step.sh),
@@ -87,11 +87,13 @@ for spec in "$@"; do
       done
       unset GAPHUFF_LIB ;;
     traffic)
+      for kv in "${a[@]:3}"; do export "$kv"; done  # optional VAR=value settings (e.g. GH_MODE=mtile)
       for c in FETCH_SIZE WRITE_SIZE; do
         step "pmc-$c-${a[1]}" 150 "$O/pmc_${c}_${a[1]}.log" timeout -s KILL 120 rocprofv3 --pmc $c --kernel-trace \
           --output-format csv -d "$O/pmc_${c}_${a[1]}" -o run -- python3 scripts/quick_one.py "$(wl "${a[2]}")" 5 || exit 1
         python3 scripts/pmc_summary.py "$O/pmc_${c}_${a[1]}" | tee -a "$O/traffic_${a[1]}.txt"
-      done ;;
+      done
+      for kv in "${a[@]:3}"; do unset "${kv%%=*}"; done ;;
     cmd)
       step "${a[1]}" "${a[2]}" "$O/${a[1]}.log" "${a[@]:3}" || true
       tail -40 "$O/${a[1]}.log" ;;
