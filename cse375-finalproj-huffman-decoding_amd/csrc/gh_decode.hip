@@ -149,6 +149,7 @@ struct gh_ctx {
   bool ws = false;
   bool ws_fb = false;              // with the canonical fallback
   uint32_t ws_k = 0, ws_kc = 0;    // write / count LUT widths
+  uint32_t ws_lgc = 0;             // log2 count-LUT copies in LDS
   uint32_t ws_nblocks = 0, ws_nranges = 0, ws_grid_c = 0;
   int ws_ns = 4;
   size_t lds_count = 0;            // dynamic LDS of the count kernel
@@ -364,6 +365,11 @@ static uint32_t ws_write_bits(const Canon& cn) {
   }
   return best;
 }
+#ifndef GH_WS_CLUT_MAX
+#define GH_WS_CLUT_MAX 0  // count-LUT bytes in LDS with its copies (0: one copy; round 5: copies at Kc 10-12
+                          // measured no faster on cfg3 than one copy at Kc 13, gpurun_out/r05am)
+#endif
+constexpr uint64_t WS_CLUT_MAX = GH_WS_CLUT_MAX;
 static int ws_ns_for(double avg_seg_bytes) {
   const double chunks = avg_seg_bytes * 64 * WS_U / 16.0 * 1.15 + 2;
   const int ns = (int)std::ceil(chunks / 64);
@@ -417,7 +423,16 @@ static int ws_setup(gh_ctx* c, double avg_seg_bytes) {
     stage = std::max<size_t>((size_t)atoll(es), (chain_worst + 15) & ~15ull) & ~15ull;
   c->stage_bytes = (uint32_t)stage;
   c->lds = lb + NW * stage;
-  c->lds_count = std::max<size_t>(4ull << kc, 64) + (fb ? FB_BYTES : 0);
+  // count LUT copies (lane l reads copy l mod 2^lgc: fewer bank conflicts on the skewed
+  // lookups), up to 32 KB in LDS; GH_WS_LGC overrides (tests, experiments)
+  c->ws_lgc = 0;
+  if (!fb) {
+    uint32_t lgc = 0;
+    while (lgc < 5 && (4ull << (kc + lgc + 1)) <= (uint64_t)WS_CLUT_MAX && 30u - kc - (lgc + 1) >= 16u) ++lgc;
+    if (const char* e = getenv("GH_WS_LGC")) lgc = (uint32_t)std::clamp(atoi(e), 0, std::max(0, 14 - (int)kc));
+    c->ws_lgc = lgc;
+  }
+  c->lds_count = std::max<size_t>(4ull << (kc + c->ws_lgc), 64) + (fb ? FB_BYTES : 0);
   c->ws_ns = ws_ns_for(avg_seg_bytes);
   if (const char* en = getenv("GH_WS_NS")) c->ws_ns = std::clamp(atoi(en), 2, 8);
   const WsKernels k = ws_kernels(kc, K, c->ws_ns, fb);
@@ -803,6 +818,7 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     wc.lut = (const uint2*)c->d_ws_lut_c;
     wc.kbits = c->ws_kc;
     wc.lut_bytes = (uint32_t)(4u << c->ws_kc);
+    wc.lgc = c->ws_lgc;
     ww = m;
     ww.lut = (const uint2*)c->d_ws_lut_w;
     ww.kbits = c->ws_k;

@@ -82,6 +82,7 @@ struct WsParams {
   unsigned long long* total;
   unsigned long long out_cap;
   uint32_t nseg, nsb, nranges, gap_nib0, first_start, kbits, lut_bytes, stage_bytes;
+  uint32_t lgc;                    // count kernel: log2 of its LUT's copies in LDS (lane l reads copy l mod 2^lgc)
   uint32_t last_end;               // != 0: end of the stream's last segment (= local segment nseg-1)
   const uint32_t* fb;              // FB kernels: canonical tables (FB_WORDS: limit16, base16, first, symbols)
   uint32_t fb_lo, fb_hi;           // their length range (minlen, maxlen)
@@ -198,11 +199,21 @@ __global__ __launch_bounds__(TBK) void gh_ws_count_kernel(const WsParams p) {
   static_assert(!FB || GL <= 2, "fallback lookups take up to 16 bits: two per window shift");
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int tid = threadIdx.x, lane = tid & 63;
-  const uint32_t sh = 30u - p.kbits;  // index bits -> byte offset of a u32 entry (the e-window's S without FB)
-  const uint32_t amask = ((1u << p.kbits) - 1u) << 2;
-  uint32_t* s_fb = (uint32_t*)(smem + p.lut_bytes);
+  // index bits -> byte offset of a u32 entry of copy lane mod 2^lgc (the e-window's S
+  // without FB; the FB kernels keep one copy)
+  const uint32_t lgc = FB ? 0u : p.lgc;
+  const uint32_t sh = 30u - p.kbits - lgc;
+  const uint32_t amask = ((1u << p.kbits) - 1u) << (2u + lgc);
+  const uint32_t laneoff = ((uint32_t)lane & ((1u << lgc) - 1u)) << 2;
+  uint32_t* s_fb = (uint32_t*)(smem + (p.lut_bytes << lgc));
   uint32_t bad = 0;
-  ws_lut_to_lds<TBK>(p, smem, tid);
+  if (lgc) {  // dword i of LDS = entry i >> lgc
+    uint32_t* sl = (uint32_t*)smem;
+    const uint32_t* g = (const uint32_t*)p.lut;
+    for (uint32_t i = tid; i < (p.lut_bytes / 4) << lgc; i += TBK) sl[i] = g[i >> lgc];
+  } else {
+    ws_lut_to_lds<TBK>(p, smem, tid);
+  }
   if constexpr (FB) ws_fb_to_lds<TBK>(p, s_fb, tid);
   if (tid == 0 && (uint32_t)(size_t)(const __attribute__((address_space(3))) uint8_t*)smem != 0u)
     atomicOr(p.status, (unsigned)GH_ST_LAYOUT);
@@ -247,7 +258,7 @@ __global__ __launch_bounds__(TBK) void gh_ws_count_kernel(const WsParams p) {
           for (int u = 0; u < U; ++u) {
             const uint32_t x = j == 0 ? v[u].d0 : __builtin_amdgcn_alignbit(v[u].d0, v[u].d1, q[u]);
             xs[u] = x;
-            asm volatile("ds_read_b32 %0, %1" : "=v"(e[u]) : "v"(FB ? (x >> sh) & amask : x & amask) : "memory");
+            asm volatile("ds_read_b32 %0, %1" : "=v"(e[u]) : "v"(FB ? (x >> sh) & amask : (x & amask) | laneoff) : "memory");
           }
           lds_wait(e);
   #pragma unroll
