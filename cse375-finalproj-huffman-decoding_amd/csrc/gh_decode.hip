@@ -285,6 +285,10 @@ static int mtile_setup(gh_ctx* c, double avg_seg_bytes) {
   const uint64_t lds_free = 160ull * 1024 - lut_b - mtile_lds_bytes(0, 0);
   const uint64_t region_max = std::min<uint64_t>(lds_free / (MT_TB / 64), 8 * 1024 + STAGE_PAD) & ~15ull;
   per_seg = std::min<uint64_t>(per_seg, (region_max - STAGE_PAD - 16) / (64ull * MT_U));
+  {  // six copy-out stores per lane (the 8-store kernel spills at lag 3) when the mean + 5 % fits
+    const uint64_t ps6 = (6144 - 16) / (64ull * MT_U);
+    if (per_seg > ps6 && (double)ps6 >= std::max(avg_seg_bytes, 1.0) * 1.05 + 1) per_seg = ps6;
+  }
   const uint64_t cap = std::max<uint64_t>(64ull * MT_U * per_seg, 64ull * maxsyms);  // piece bytes staged at once
   if (STAGE_PAD + cap + 16 > region_max) return GH_OK;
   c->mt_ns = cap + 16 <= 4096 ? 4 : cap + 16 <= 6144 ? 6 : 8;  // the copy-out's chunks cover a piece
@@ -619,13 +623,14 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
       if (force_tile && !c->tile) return fail(GH_E_HIP, "GH_MODE=tile: the tile kernel does not fit a CU");
     }
     // the two-pass tile kernel: codes of 2..12-bit codewords the single-pass one does not
-    // take (GH_MTILE=1; GH_MODE=mtile forces it)
+    // take (cfg3's r = 0.9 codes; GH_MTILE=0 leaves them to the wave split, GH_MODE=mtile
+    // forces it)
     const bool multi = cn.minlen >= 2 && cn.maxlen <= 12 && kraft16(cn) == 65536;
     if (force_mt && !multi)
       return fail(GH_E_ARG, "GH_MODE=mtile: the code is not for the two-pass tile kernel (complete, 2..12 bits)");
     static const bool mt_on = [] {
       const char* e = getenv("GH_MTILE");
-      return e && e[0] == '1';
+      return !(e && e[0] == '0');
     }();
     if (!c->tile && multi && (force_mt || (mt_on && !force_ws && !force_tile))) {
       if ((rc = mtile_setup(c, avg))) return rc;

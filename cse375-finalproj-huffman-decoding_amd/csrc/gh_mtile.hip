@@ -58,7 +58,7 @@ constexpr int MT_LAG = GH_MT_LAG;
                       // 4 << K bytes after the write table) instead of the write table's high words
 #endif
 #ifndef GH_MT_WOR
-#define GH_MT_WOR 1  // write pass: 1 ORs into zeroed staging (two aligned ds_or_b32 per lookup,
+#define GH_MT_WOR 2  // write pass: 1 ORs into zeroed staging (two aligned ds_or_b32 per lookup,
                      // the copy-out re-zeroes), 2 the same with the bytes gathered into
                      // aligned dwords first (one ds_or_b32 per lookup), 0 unaligned
                      // ds_write_b32 + head restore
@@ -226,10 +226,12 @@ __device__ __forceinline__ void mt_write(uint32_t (&e)[U][5], const uint32_t (&o
     }
   }
   // every lane's lookups are done: the head bytes over the previous segment's overrun
-  // and end writes (in wave order: after them)
+  // and end writes (in wave order: after them); (GH_MT_WOR 2) the pending dword a last
+  // lookup moved past
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     if (!GH_MT_WOR && n[u]) lds_st32(o[u], head[u]);
+    if (GH_MT_WOR == 2) asm volatile("ds_or_b32 %0, %1" ::"v"(dptr[u]), "v"(alo[u]) : "memory");
   }
 }
 
