@@ -139,6 +139,7 @@ struct gh_ctx {
   uint32_t tile_minl = 4, tile_u = TILE_U;     // kernel shape (tile_kernel_for), segments per lane
   uint32_t idle_block = 0xFFFFFFFFu;           // GH_TILE_IDLE experiments: a block that exits at once
   bool mtile = false;              // the two-pass tile kernel (gh_mtile.hip; c->tile is set too)
+  uint32_t mt_kc = 0;              // its count table's width
   int mt_gl = 2, mt_ns = 4;        // its lookups per window shift, stores per copy-out
   uint32_t* d_lut_t = nullptr;
   uint4* d_stamps = nullptr;       // GH_TILE_STAMPS builds only
@@ -281,7 +282,17 @@ static int mtile_setup(gh_ctx* c, double avg_seg_bytes) {
   uint64_t per_seg = std::min<uint64_t>(maxsyms, (uint64_t)std::ceil(std::max(avg_seg_bytes, 1.0) * scapf + 1));
   if (const char* e = getenv("GH_TILE_SCAP")) per_seg = std::min<uint64_t>(maxsyms, (uint64_t)std::max(1, atoi(e)));
   // at most what the LDS (LUT + 16 regions + slots) and the copy-out's 8 x 64 chunks hold
-  const uint64_t lut_b = (GH_MT_CLUT ? 12ull : 8ull) << K;  // write table (+ count table)
+  // count table width: wider than the write table's (more codewords per lookup) where
+  // the LDS and a window shift allow it (GL lookups of Kc bits within 31 bits)
+  uint32_t Kc = K;
+  if (GH_MT_CLUT) {
+    const int gl = lookups_per_shift(K);
+    Kc = std::min<uint32_t>(13, 31 / gl);
+    if (const char* e = getenv("GH_MT_KC")) Kc = (uint32_t)std::clamp(atoi(e), (int)K, (int)std::min(14, 31 / gl));
+    Kc = std::max(Kc, K);
+  }
+  c->mt_kc = Kc;
+  const uint64_t lut_b = GH_MT_CLUT ? (8ull << K) + (4ull << Kc) : 8ull << K;  // write table (+ count table)
   const uint64_t lds_free = 160ull * 1024 - lut_b - mtile_lds_bytes(0, 0);
   const uint64_t region_max = std::min<uint64_t>(lds_free / (MT_TB / 64), 8 * 1024 + STAGE_PAD) & ~15ull;
   per_seg = std::min<uint64_t>(per_seg, (region_max - STAGE_PAD - 16) / (64ull * MT_U));
@@ -302,15 +313,18 @@ static int mtile_setup(gh_ctx* c, double avg_seg_bytes) {
   pc = std::min(pc, 2);  // (as tile_setup: the occupancy query can answer one too many)
   if (pc < 1) return GH_OK;
   std::vector<uint64_t> lt = multi_lut(cn, K);
-  if (GH_MT_CLUT) {  // the count table (u32 {b | start mask << 16}, every codeword of the window) after it
-    std::vector<uint32_t> lc(1u << K);
-    for (uint32_t i = 0; i < (1u << K); ++i) {
+  if (GH_MT_CLUT) {  // the count table (u32 {b | start mask << 16}, every codeword of the window)
+    std::vector<uint32_t> lc(1u << Kc);
+    for (uint32_t i = 0; i < (1u << Kc); ++i) {
       uint32_t n = 0, m = 0;
-      const uint32_t b = window_codewords(cn, i, K, 32, &n, nullptr, &m);
+      const uint32_t b = window_codewords(cn, i, Kc, 32, &n, nullptr, &m);
       lc[i] = b | ((n ? (1u | (m << 1)) & ((1u << b) - 1u) : 0u) << 16);
     }
-    lt.resize((12ull << K) / 8);
-    std::memcpy(lt.data() + (1u << K), lc.data(), 4ull << K);
+    std::vector<uint64_t> both(lut_b / 8);
+    const bool cfirst = (4ull << Kc) > (8ull << K);  // the larger table first (gh_mtile.hip)
+    std::memcpy((uint8_t*)both.data() + (cfirst ? 0 : 8ull << K), lc.data(), 4ull << Kc);
+    std::memcpy((uint8_t*)both.data() + (cfirst ? 4ull << Kc : 0), lt.data(), 8ull << K);
+    lt.swap(both);
   }
   GH_HIP(hipMalloc(&c->d_lut_t, lut_b));
   GH_HIP(hipMemcpy(c->d_lut_t, lt.data(), lut_b, hipMemcpyHostToDevice));
@@ -855,6 +869,7 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     t.epoch = c->epoch;
     t.lut_bytes = (uint32_t)c->lut_bytes;
     t.stage_bytes = c->stage_bytes;
+    t.kbits_c = c->mt_kc;
     t.stamps = c->d_stamps;
     t.tstamps = c->d_stamps ? (unsigned long long*)((uint8_t*)c->d_stamps + 32ull * c->grid * 2 * 128) : nullptr;
     t.idle_block = c->idle_block;

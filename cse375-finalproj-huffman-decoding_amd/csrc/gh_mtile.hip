@@ -137,7 +137,7 @@ __device__ __forceinline__ void mt_count(uint32_t (&e)[U][5], const int (&R0)[U]
 // the head stores, above).  A chain with n = 0 writes nothing.
 template <int U, int GL>
 __device__ __forceinline__ void mt_write(uint32_t (&e)[U][5], const uint32_t (&o)[U], const uint32_t (&n)[U],
-                                         uint32_t amask) {
+                                         uint32_t amask, uint32_t wbase) {
   uint32_t ptr[U], end[U], head[U];
   uint32_t alo[U], ahi[U], fill[U], dptr[U];  // (GH_MT_WOR 2) pending bytes, their count, dword address
   int rem[U];
@@ -163,7 +163,7 @@ __device__ __forceinline__ void mt_write(uint32_t (&e)[U][5], const uint32_t (&o
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const uint32_t x = j == 0 ? e[u][0] : __builtin_amdgcn_alignbit(e[u][0], e[u][1], q[u]);
-        ent[u] = lds_u64_nowait(x & amask);
+        ent[u] = lds_u64_nowait((x & amask) | wbase);
       }
       lds_wait(ent);
 #pragma unroll
@@ -276,11 +276,15 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
   }
   const uint32_t S = 29u - p.kbits;                        // write pass: u64 entries
   const uint32_t amask = ((1u << p.kbits) - 1u) << 3;
-  // count pass: its own u32 table after the write table (GH_MT_CLUT), or the write
-  // table's high words
-  const uint32_t Sc = GH_MT_CLUT ? 30u - p.kbits : S;
-  const uint32_t amask_c = GH_MT_CLUT ? ((1u << p.kbits) - 1u) << 2 : amask;
-  const uint32_t cbase = GH_MT_CLUT ? 8u << p.kbits : 4u;
+  // count pass: its own u32 table of width Kc (GH_MT_CLUT), the larger of the two
+  // tables first so that each base ORs into its table's addresses; or the write table's
+  // high words
+  const uint32_t Kc = GH_MT_CLUT ? p.kbits_c : p.kbits;
+  const uint32_t Sc = GH_MT_CLUT ? 30u - Kc : S;
+  const uint32_t amask_c = GH_MT_CLUT ? ((1u << Kc) - 1u) << 2 : amask;
+  const bool cfirst = GH_MT_CLUT && (4u << Kc) > (8u << p.kbits);
+  const uint32_t cbase = !GH_MT_CLUT ? 4u : cfirst ? 0u : 8u << p.kbits;
+  const uint32_t wbase = cfirst ? 4u << Kc : 0u;
   check_lds_base(smem, p.status);
   const uint32_t G = D, b = blockIdx.x - 1;
   const uint32_t nseg = (uint32_t)p.nseg;
@@ -417,7 +421,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
       uint32_t o[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) o[u] = region + STAGE_PAD + hpos[L - 1][u];
-      mt_write<U, GL>(he[L - 1], o, hcnt[L - 1], amask);
+      mt_write<U, GL>(he[L - 1], o, hcnt[L - 1], amask, wbase);
     }
     // ---- the prefix of tile k-1 -> this wave's piece's output offset (gh_tile.hip) --------
     unsigned long long goff = 0;
@@ -495,7 +499,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
         for (int v = 0; v < U; ++v)
 #pragma unroll
           for (int i = 0; i < 5; ++i) ew[v][i] = he[L - 1][v][i];
-        mt_write<U, GL>(ew, o, nn, amask);
+        mt_write<U, GL>(ew, o, nn, amask, wbase);
         const unsigned long long gu = goff + c0;
         const uint32_t nu = (!got || gu >= p.out_cap) ? 0u : (uint32_t)min<unsigned long long>(ct, p.out_cap - gu);
         tile_v4u cv[NS];
