@@ -66,11 +66,8 @@ WORKLOADS = {
 # (mode, path) -> the kernels one decode launches (rocprofv3 names); path -1 = any
 KERNEL_NAMES = {
     (1, 4): "gh::gh_ws_count_kernel + gh::gh_ws_scan_kernel + gh::gh_ws_write_kernel",
-    (1, 3): "gh::gh_ms_count_kernel + gh::gh_ms_write_kernel",
-    (1, -1): "gh::gh_count_kernel + gh::gh_write_kernel",
     (2, -1): "gh::gh_tile_kernel",
-    (3, -1): "gh::gh_ftile_kernel",
-    (0, -1): "gh::gh_decode_kernel",
+    (4, -1): "gh::gh_mtile_kernel",
 }
 
 
