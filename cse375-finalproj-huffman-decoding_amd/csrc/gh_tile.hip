@@ -512,6 +512,46 @@ __device__ __forceinline__ unsigned long long poll_granule(const TileParams& p, 
   }
 }
 
+#ifndef GH_TILE_PPOLL
+#define GH_TILE_PPOLL 1  // loads in flight per poll (the leader's and the decoders' prefix polls); 2-3 measured
+                         // slower on cfg4 (0.440 vs 0.433 ms steady, gpurun_out/r05at)
+#endif
+// The same with PN loads in flight, issued a few hundred cycles apart and re-issued as each
+// is checked (loads complete in order): a granule that becomes visible while a load is
+// in flight is seen by the next load to return, not a whole round trip later.
+template <int PN>
+__device__ __forceinline__ unsigned long long poll_granule_pipe(const TileParams& p, unsigned long long* g,
+                                                                uint32_t flag) {
+  if constexpr (PN <= 1) {
+    return poll_granule(p, g, flag);
+  } else {
+    unsigned long long v[PN];
+#pragma unroll
+    for (int i = 0; i < PN; ++i) {
+      v[i] = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (i + 1 < PN) __builtin_amdgcn_s_sleep(8);
+    }
+    unsigned long long t0 = 0;
+    for (uint32_t spins = 1;; ++spins) {
+#pragma unroll
+      for (int i = 0; i < PN; ++i) {
+        if (granule_ok(p, v[i], flag)) return v[i];
+        v[i] = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if ((spins & 15u) == 0u) {
+        if (__hip_atomic_load(p.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & GH_ST_TIMEOUT) return 0;
+        const unsigned long long t = wall_clock64();
+        if (t0 == 0) {
+          t0 = t;
+        } else if (t - t0 > 400000000ull) {
+          atomicOr(p.status, (unsigned)GH_ST_TIMEOUT);
+          return 0;
+        }
+      }
+    }
+  }
+}
+
 // The round leader (workgroup 0): for every round r of D decoding workgroups' tiles, wait
 // for the round's aggregates (thread t takes the A = ceil(D / TB) <= LEAD_A consecutive
 // tiles t*A .. t*A + A - 1 of the round), scan them and publish each tile's global
@@ -537,7 +577,7 @@ __device__ __forceinline__ void tile_round_leader(const TileParams& p, uint32_t 
         unsigned long long g = __hip_atomic_load(&p.granules[t0 + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (!granule_ok(p, g, 1)) {
           atomicAdd(p.stats + 1, 1ull);
-          g = poll_granule(p, &p.granules[t0 + j], 1);
+          g = poll_granule_pipe<GH_TILE_PPOLL>(p, &p.granules[t0 + j], 1);
         }
         v[i] = (uint32_t)(g & GRAN_VMASK);  // a tile holds < 2^32 symbols
       }
@@ -829,21 +869,40 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
           polled = true;
           if (wid == 0 && lane == 0) atomicAdd(p.stats, 1ull);
           unsigned long long t0w = 0;
+          // GH_TILE_PPOLL loads in flight (poll_granule_pipe), each checked in turn after
+          // the workgroup's LDS post
+          constexpr int PN = GH_TILE_PPOLL < 1 ? 1 : GH_TILE_PPOLL;
+          unsigned long long pv[PN];
+#pragma unroll
+          for (int i = 0; i < PN; ++i) {
+            pv[i] = __hip_atomic_load(pf2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (i + 1 < PN) __builtin_amdgcn_s_sleep(4);
+          }
           for (uint32_t spins = 1;; ++spins) {
-            if (lds_ld_u32(ptile_lds + 4u * slot2) == t2) {
-              asm volatile("" ::: "memory");
-              g = s_pfx[slot2];
-              break;
-            }
-            g = rfl_u64(__hip_atomic_load(pf2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            if (granule_ok(p, g, 2)) {
-              if (lane == 0) {  // post: the value, then its tile (LDS order)
-                s_pfx[slot2] = g;
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                lds_st_u32(ptile_lds + 4u * slot2, t2);
+            bool found = false;
+#pragma unroll
+            for (int i = 0; i < PN; ++i) {
+              if (!found) {
+                if (lds_ld_u32(ptile_lds + 4u * slot2) == t2) {
+                  asm volatile("" ::: "memory");
+                  g = s_pfx[slot2];
+                  found = true;
+                } else {
+                  g = rfl_u64(pv[i]);
+                  if (granule_ok(p, g, 2)) {
+                    if (lane == 0) {  // post: the value, then its tile (LDS order)
+                      s_pfx[slot2] = g;
+                      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                      lds_st_u32(ptile_lds + 4u * slot2, t2);
+                    }
+                    found = true;
+                  } else {
+                    pv[i] = __hip_atomic_load(pf2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                  }
+                }
               }
-              break;
             }
+            if (found) break;
             if ((spins & 63u) == 0u) {  // bounded like poll_granule: 4 s of the 100 MHz clock
               if (__hip_atomic_load(p.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & GH_ST_TIMEOUT) break;
               const unsigned long long t = wall_clock64();
@@ -854,7 +913,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
                 break;
               }
             }
-            __builtin_amdgcn_s_sleep(1);
+            if (PN == 1) __builtin_amdgcn_s_sleep(1);
           }
           got = granule_ok(p, g, 2);  // false only after a timeout (then nothing is written)
         }
