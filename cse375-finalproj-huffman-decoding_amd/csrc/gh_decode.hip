@@ -76,14 +76,16 @@ static const void* tile_kernel_for(uint32_t minlen, uint32_t g) {
 }
 
 // Two-pass tile kernel by lookups per window shift and 16-byte stores per copy-out.
-template <int GL>
+template <int GL, bool FB>
 static const void* mtile_ns(int ns) {
-  return ns <= 4 ? (const void*)gh_mtile_kernel<MT_TB, GL, 4>
-       : ns <= 6 ? (const void*)gh_mtile_kernel<MT_TB, GL, 6>
-                 : (const void*)gh_mtile_kernel<MT_TB, GL, 8>;
+  return ns <= 4 ? (const void*)gh_mtile_kernel<MT_TB, GL, 4, FB>
+       : ns <= 6 ? (const void*)gh_mtile_kernel<MT_TB, GL, 6, FB>
+                 : (const void*)gh_mtile_kernel<MT_TB, GL, 8, FB>;
 }
-static const void* mtile_kernel_for(int gl, int ns) {
-  return gl >= 4 ? mtile_ns<4>(ns) : gl == 3 ? mtile_ns<3>(ns) : mtile_ns<2>(ns);
+// fb: codewords longer than the tables (K = 12, GL = 2) through the canonical fallback
+static const void* mtile_kernel_for(int gl, int ns, bool fb = false) {
+  if (fb) return mtile_ns<2, true>(ns);
+  return gl >= 4 ? mtile_ns<4, false>(ns) : gl == 3 ? mtile_ns<3, false>(ns) : mtile_ns<2, false>(ns);
 }
 
 struct WsKernels {
@@ -139,6 +141,7 @@ struct gh_ctx {
   uint32_t tile_minl = 4, tile_u = TILE_U;     // kernel shape (tile_kernel_for), segments per lane
   uint32_t idle_block = 0xFFFFFFFFu;           // GH_TILE_IDLE experiments: a block that exits at once
   bool mtile = false;              // the two-pass tile kernel (gh_mtile.hip; c->tile is set too)
+  bool mt_fb = false;              // ... with the canonical fallback (codewords longer than its tables)
   uint32_t mt_kc = 0;              // its count table's width
   int mt_gl = 2, mt_ns = 4;        // its lookups per window shift, stores per copy-out
   uint32_t* d_lut_t = nullptr;
@@ -189,6 +192,7 @@ static void free_shard(gh_ctx* c) {
   c->d_rng_off = nullptr;
   c->tile = false;
   c->mtile = false;
+  c->mt_fb = false;
   c->ws = false;
   c->loaded = false;
 }
@@ -275,7 +279,10 @@ static uint32_t ws_write_bits(const Canon& cn);
 static int mtile_setup(gh_ctx* c, double avg_seg_bytes) {
   const Canon& cn = c->canon;
   const uint32_t K = ws_write_bits(cn);
-  if (K < cn.maxlen) return GH_OK;
+  // codewords longer than the tables (up to 16 bits) take the canonical fallback, with
+  // two lookups per window shift (2 x 12 + 16 > 32 otherwise)
+  const bool fb = K < cn.maxlen;
+  if (fb && (K != 12 || cn.maxlen > 16)) return GH_OK;
   const uint32_t maxsyms = (128 + cn.minlen - 1) / cn.minlen;  // <= 64
   double scapf = 1.12;
   if (const char* e = getenv("GH_TILE_SCAPF")) scapf = std::clamp(atof(e), 0.5, 4.0);
@@ -292,7 +299,8 @@ static int mtile_setup(gh_ctx* c, double avg_seg_bytes) {
     Kc = std::max(Kc, K);
   }
   c->mt_kc = Kc;
-  const uint64_t lut_b = GH_MT_CLUT ? (8ull << K) + (4ull << Kc) : 8ull << K;  // write table (+ count table)
+  const uint64_t lut_b = (GH_MT_CLUT ? (8ull << K) + (4ull << Kc) : 8ull << K)  // write table (+ count table)
+                         + (fb ? (uint64_t)FB_BYTES : 0);                         // (+ fallback tables)
   const uint64_t lds_free = 160ull * 1024 - lut_b - mtile_lds_bytes(0, 0);
   const uint64_t region_max = std::min<uint64_t>(lds_free / (MT_TB / 64), 8 * 1024 + STAGE_PAD) & ~15ull;
   per_seg = std::min<uint64_t>(per_seg, (region_max - STAGE_PAD - 16) / (64ull * MT_U));
@@ -305,7 +313,8 @@ static int mtile_setup(gh_ctx* c, double avg_seg_bytes) {
   c->mt_ns = cap + 16 <= 4096 ? 4 : cap + 16 <= 6144 ? 6 : 8;  // the copy-out's chunks cover a piece
   c->stage_bytes = (uint32_t)((STAGE_PAD + cap + 16 + 15) & ~15ull);  // + the write overrun
   c->mt_gl = lookups_per_shift(K);
-  const void* kern = mtile_kernel_for(c->mt_gl, c->mt_ns);
+  c->mt_fb = fb;
+  const void* kern = mtile_kernel_for(c->mt_gl, c->mt_ns, fb);
   c->lut_bytes = lut_b;
   c->lds = mtile_lds_bytes(c->lut_bytes, c->stage_bytes);
   int pc = 0;
@@ -325,6 +334,13 @@ static int mtile_setup(gh_ctx* c, double avg_seg_bytes) {
     std::memcpy((uint8_t*)both.data() + (cfirst ? 0 : 8ull << K), lc.data(), 4ull << Kc);
     std::memcpy((uint8_t*)both.data() + (cfirst ? 4ull << Kc : 0), lt.data(), 8ull << K);
     lt.swap(both);
+  }
+  if (fb) {  // the canonical tables after the LUTs (the kernel reads the last FB_BYTES)
+    uint32_t fbt[FB_WORDS];
+    fallback_tables(cn, fbt);
+    const size_t at = lut_b - FB_BYTES;
+    lt.resize(lut_b / 8, 0);
+    std::memcpy((uint8_t*)lt.data() + at, fbt, sizeof(fbt));
   }
   GH_HIP(hipMalloc(&c->d_lut_t, lut_b));
   GH_HIP(hipMemcpy(c->d_lut_t, lt.data(), lut_b, hipMemcpyHostToDevice));
@@ -531,7 +547,8 @@ extern "C" int gh_ctx_create(int device, gh_ctx** out) {
       (void)hipFuncSetAttribute(tile_kernel_for(ml, gv), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   for (int gl : {2, 3, 4})
     for (int ns : {4, 6, 8})
-      (void)hipFuncSetAttribute(mtile_kernel_for(gl, ns), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      for (bool fb : {false, true})
+        (void)hipFuncSetAttribute(mtile_kernel_for(gl, ns, fb), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   (void)hipGetLastError();
   *out = c;
   return GH_OK;
@@ -639,9 +656,9 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
     // the two-pass tile kernel: codes of 2..12-bit codewords the single-pass one does not
     // take (cfg3's r = 0.9 codes; GH_MTILE=0 leaves them to the wave split, GH_MODE=mtile
     // forces it)
-    const bool multi = cn.minlen >= 2 && cn.maxlen <= 12 && kraft16(cn) == 65536;
+    const bool multi = cn.minlen >= 2 && cn.maxlen <= 16 && kraft16(cn) == 65536;
     if (force_mt && !multi)
-      return fail(GH_E_ARG, "GH_MODE=mtile: the code is not for the two-pass tile kernel (complete, 2..12 bits)");
+      return fail(GH_E_ARG, "GH_MODE=mtile: the code is not for the two-pass tile kernel (complete, 2..16 bits)");
     static const bool mt_on = [] {
       const char* e = getenv("GH_MTILE");
       return !(e && e[0] == '0');
@@ -870,10 +887,11 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     t.lut_bytes = (uint32_t)c->lut_bytes;
     t.stage_bytes = c->stage_bytes;
     t.kbits_c = c->mt_kc;
+    t.fb_hi = c->canon.maxlen;
     t.stamps = c->d_stamps;
     t.tstamps = c->d_stamps ? (unsigned long long*)((uint8_t*)c->d_stamps + 32ull * c->grid * 2 * 128) : nullptr;
     t.idle_block = c->idle_block;
-    const void* kern = c->mtile ? mtile_kernel_for(c->mt_gl, c->mt_ns) : tile_kernel_for(c->tile_minl, c->tile_g);
+    const void* kern = c->mtile ? mtile_kernel_for(c->mt_gl, c->mt_ns, c->mt_fb) : tile_kernel_for(c->tile_minl, c->tile_g);
     static thread_local void* ta[1];
     static thread_local TileParams tp;
     tp = t;

@@ -77,6 +77,19 @@ __device__ __forceinline__ void win_shift5(uint32_t (&e)[5], uint32_t q) {
   e[4] = __builtin_amdgcn_alignbit(e[4], 0u, q);
 }
 
+// Codes longer than the tables (FB): a codeword longer than the table width has no entry
+// (b = 0 / n = 0); its 16 bits are taken from the e-window (S bits below the lookup
+// position) and decoded canonically from the LDS tables (gh_wsplit.hip's ws_canon;
+// codes here are complete, so every pattern decodes).
+struct MtFb {
+  const uint32_t* s_fb;
+  uint32_t lo, hi;  // lengths searched: table width + 1 .. maxlen
+};
+__device__ __forceinline__ uint32_t mt_canon(const MtFb& fb, uint32_t x, uint32_t y, uint32_t S) {
+  uint32_t bad = 0;
+  return ws_canon(fb.s_fb, __builtin_amdgcn_alignbit(x, y, 32u - S) >> 16, fb.lo, fb.hi, bad);  // (sym << 8) | len
+}
+
 // LDS: LUT (8 << K bytes), one staging region per wave, the per-tile wave totals /
 // offsets / arrival counters / prefixes (TILE_SLOTS tiles), leader wave totals.
 inline size_t mtile_lds_bytes(size_t lut_bytes, size_t stage_bytes) {
@@ -87,9 +100,9 @@ inline size_t mtile_lds_bytes(size_t lut_bytes, size_t stage_bytes) {
 // Count pass of U segments per lane on e-windows (S = 29 - K, u64 entries): codewords
 // that start before the segment end, R = 128 - start bits away.  GL lookups per window
 // shift (GL * K <= 24 bits: rm, recomputed per group from R, covers the group's starts).
-template <int U, int GL>
+template <int U, int GL, bool FB = false>
 __device__ __forceinline__ void mt_count(uint32_t (&e)[U][5], const int (&R0)[U], uint32_t (&cnt)[U], uint32_t amask,
-                                         uint32_t cbase) {
+                                         uint32_t cbase, const MtFb& fb = MtFb{}, uint32_t Sc = 0) {
   int R[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
@@ -112,6 +125,16 @@ __device__ __forceinline__ void mt_count(uint32_t (&e)[U][5], const int (&R0)[U]
         hi[u] = lds_u32_nowait((x & amask) | cbase);  // the count entry (or the write entry's high word)
       }
       lds_wait(hi);
+      if constexpr (FB) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if ((hi[u] & 31u) == 0u) {  // a codeword longer than the table: one codeword, start bit 0
+            const uint32_t x = j == 0 ? e[u][0] : __builtin_amdgcn_alignbit(e[u][0], e[u][1], q[u]);
+            const uint32_t y = j == 0 ? e[u][1] : __builtin_amdgcn_alignbit(e[u][1], e[u][2], q[u]);
+            hi[u] = (mt_canon(fb, x, y, Sc) & 31u) | (1u << 16);
+          }
+        }
+      }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         uint32_t m;
@@ -135,9 +158,9 @@ __device__ __forceinline__ void mt_count(uint32_t (&e)[U][5], const int (&R0)[U]
 
 // Write pass: the n[u] codewords of each segment to LDS bytes [o[u], o[u] + n[u]) (then
 // the head stores, above).  A chain with n = 0 writes nothing.
-template <int U, int GL>
+template <int U, int GL, bool FB = false>
 __device__ __forceinline__ void mt_write(uint32_t (&e)[U][5], const uint32_t (&o)[U], const uint32_t (&n)[U],
-                                         uint32_t amask, uint32_t wbase) {
+                                         uint32_t amask, uint32_t wbase, const MtFb& fb = MtFb{}, uint32_t Sw = 0) {
   uint32_t ptr[U], end[U], head[U];
   uint32_t alo[U], ahi[U], fill[U], dptr[U];  // (GH_MT_WOR 2) pending bytes, their count, dword address
   int rem[U];
@@ -166,6 +189,17 @@ __device__ __forceinline__ void mt_write(uint32_t (&e)[U][5], const uint32_t (&o
         ent[u] = lds_u64_nowait((x & amask) | wbase);
       }
       lds_wait(ent);
+      if constexpr (FB) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if ((ent[u].y & 0x700u) == 0u) {  // n = 0: a codeword longer than the table
+            const uint32_t x = j == 0 ? e[u][0] : __builtin_amdgcn_alignbit(e[u][0], e[u][1], q[u]);
+            const uint32_t y = j == 0 ? e[u][1] : __builtin_amdgcn_alignbit(e[u][1], e[u][2], q[u]);
+            const uint32_t r = mt_canon(fb, x, y, Sw);
+            ent[u] = make_uint2(r >> 8, (r & 31u) | (1u << 8));
+          }
+        }
+      }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (GH_MT_WOR == 2) {
@@ -244,7 +278,7 @@ __device__ __forceinline__ void mt_zero(uint32_t region, uint32_t n, int lane) {
     asm volatile("ds_write_b128 %0, %1" ::"v"(region + 16u * c), "v"(tile_v4u{0, 0, 0, 0}) : "memory");
 }
 
-template <int TB, int GL, int NS>
+template <int TB, int GL, int NS, bool FB = false>
 __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void gh_mtile_kernel(const TileParams p) {
   constexpr int U = MT_U;
   constexpr int NW = TB / 64;
@@ -285,6 +319,8 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
   const bool cfirst = GH_MT_CLUT && (4u << Kc) > (8u << p.kbits);
   const uint32_t cbase = !GH_MT_CLUT ? 4u : cfirst ? 0u : 8u << p.kbits;
   const uint32_t wbase = cfirst ? 4u << Kc : 0u;
+  // (FB) the canonical tables: the last FB_BYTES of the LUT area
+  const MtFb fb{(const uint32_t*)(smem + p.lut_bytes - (FB ? FB_BYTES : 0)), p.kbits + 1u, p.fb_hi};
   check_lds_base(smem, p.status);
   const uint32_t G = D, b = blockIdx.x - 1;
   const uint32_t nseg = (uint32_t)p.nseg;
@@ -377,7 +413,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
 #pragma unroll
         for (int u = 0; u < U; ++u) cnt[u] = R[u] > 0 ? 40u : 0u;
       } else {
-        mt_count<U, GL>(e, R, cnt, amask_c, cbase);
+        mt_count<U, GL, FB>(e, R, cnt, amask_c, cbase, fb, Sc);
       }
     }
     const unsigned long long gp = __hip_atomic_load(pf2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -421,7 +457,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
       uint32_t o[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) o[u] = region + STAGE_PAD + hpos[L - 1][u];
-      mt_write<U, GL>(he[L - 1], o, hcnt[L - 1], amask, wbase);
+      mt_write<U, GL, FB>(he[L - 1], o, hcnt[L - 1], amask, wbase, fb, S);
     }
     // ---- the prefix of tile k-1 -> this wave's piece's output offset (gh_tile.hip) --------
     unsigned long long goff = 0;
@@ -499,7 +535,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
         for (int v = 0; v < U; ++v)
 #pragma unroll
           for (int i = 0; i < 5; ++i) ew[v][i] = he[L - 1][v][i];
-        mt_write<U, GL>(ew, o, nn, amask, wbase);
+        mt_write<U, GL, FB>(ew, o, nn, amask, wbase, fb, S);
         const unsigned long long gu = goff + c0;
         const uint32_t nu = (!got || gu >= p.out_cap) ? 0u : (uint32_t)min<unsigned long long>(ct, p.out_cap - gu);
         tile_v4u cv[NS];

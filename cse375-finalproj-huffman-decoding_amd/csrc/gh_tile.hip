@@ -103,6 +103,7 @@ struct TileParams {
   unsigned int idle_block;       // a block that exits at once (>= grid: none)
   unsigned int stage_bytes;      // one wave's staging region (16 + its piece + margin, a multiple of 16)
   unsigned int kbits_c;          // (gh_mtile.hip) the count table's width
+  unsigned int fb_hi;            // (gh_mtile.hip, codes longer than the tables) the longest codeword
   uint4* stamps;                 // GH_TILE_STAMPS builds: [grid][2 waves][128 iterations][2] phase deltas
   unsigned long long* tstamps;   // GH_TILE_STAMPS builds: 100 MHz times: [ntiles] aggregate left, [ntiles]
                                  // prefix obtained by wave 0 (bit 63: polled), [rounds] round published

@@ -73,12 +73,30 @@ def test_mtile_small_codes(gpu, orc, mtile):
         gpu.decode(gpu.encode(two))
 
 
+@pytest.mark.parametrize("q,n", [(0.7, 300_001), (0.7, 3_000_017), (0.75, 1_000_003)])
+def test_mtile_long_codes_fallback(gpu, orc, monkeypatch, q, n):
+    """Codes of 2..16-bit codewords (geometric byte distributions): the codewords longer
+    than the 12-bit tables go through the canonical fallback inside the kernel; the
+    launcher picks the two-pass kernel for them by default."""
+    rng = np.random.default_rng(int(q * 100) + n)
+    p = q ** np.arange(256, dtype=np.float64)
+    p /= p.sum()
+    data = rng.choice(256, size=n, p=p).astype(np.uint8)
+    img = gpu.encode(data)
+    lens = [l for _, l in gpu.parse(img).symbols]
+    assert min(lens) >= 2 and max(lens) > 12
+    _check(gpu, orc, data)
+    rep = _report(gpu, img)
+    assert gpu.MODE_NAMES[rep.mode] == "mtile" and rep.status == 0
+
+
 def test_mtile_refuses_fallback_codes(gpu, mtile):
-    """Codes longer than the tables (16-bit codewords) need the wave split's canonical
-    fallback: GH_MODE=mtile fails loudly at load."""
+    """Codes with a 1-bit codeword (here also 16-bit ones) stay with the wave split:
+    GH_MODE=mtile fails loudly at load."""
     counts = [max(1, int(2 ** (24 - 0.9 * i))) for i in range(40)]
     data = np.repeat(np.arange(40, dtype=np.uint8), counts)
     s = gpu.parse(gpu.encode(data))
+    assert min(l for _, l in s.symbols) == 1 and max(l for _, l in s.symbols) == 16
     with gpu.Decoder(0) as d:
         with pytest.raises(gpu.GapHuffError):
             d.load(s)
