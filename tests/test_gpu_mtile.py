@@ -37,8 +37,8 @@ def _complete(syms):
     return sum(2.0 ** -l for _, l in syms) == 1.0
 
 
-def _takes(syms):  # the kernel's codes: complete, codewords of 2..12 bits
-    return _complete(syms) and max(l for _, l in syms) <= 12 and min(l for _, l in syms) >= 2
+def _takes(syms):  # the kernel's codes: complete, codewords of 2..16 bits (> 12 through its fallback)
+    return _complete(syms) and max(l for _, l in syms) <= 16 and min(l for _, l in syms) >= 2
 
 
 @pytest.mark.parametrize("r", [0.1, 0.5, 0.9, 0.999])
