@@ -1,5 +1,5 @@
 """GPU parity tests of the two-pass tile kernel (gh_mtile.hip, GH_MODE=mtile): complete
-codes of 2..12-bit codewords (BASELINE's r = 0.9 codes, and the r = 0.5 / 0.1 codes too
+codes of 2..16-bit codewords (those above 12 bits through a canonical fallback; BASELINE's r = 0.9 codes, and the r = 0.5 / 0.1 codes too
 when forced) decoded by one persistent kernel that reads the payload once: a count pass
 and, one tile later, a write pass over the same register-resident words.  Bit-exact
 against the CPU oracle and the original input (reference: decoder/src/decoder.cu:454-730,
