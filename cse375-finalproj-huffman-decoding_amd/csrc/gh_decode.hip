@@ -80,9 +80,10 @@ template <int GL, bool FB>
 static const void* mtile_ns(int ns) {
   return ns <= 4 ? (const void*)gh_mtile_kernel<MT_TB, GL, 4, FB>
        : ns <= 6 ? (const void*)gh_mtile_kernel<MT_TB, GL, 6, FB>
-                 : (const void*)gh_mtile_kernel<MT_TB, GL, 8, FB>;
+       : ns <= 8 ? (const void*)gh_mtile_kernel<MT_TB, GL, 8, FB>
+                 : (const void*)gh_mtile_kernel<MT_TB, GL, 5, FB, 2>;  // (10: two copy-out parts of 5 x 64 chunks)
 }
-// fb: codewords longer than the tables (K = 12, GL = 2) through the canonical fallback
+// fb: codewords longer than the tables (K = 11..12, GL = 2) through the canonical fallback
 static const void* mtile_kernel_for(int gl, int ns, bool fb = false) {
   if (fb) return mtile_ns<2, true>(ns);
   return gl >= 4 ? mtile_ns<4, false>(ns) : gl == 3 ? mtile_ns<3, false>(ns) : mtile_ns<2, false>(ns);
@@ -269,21 +270,26 @@ static int tile_setup(gh_ctx* c, uint32_t K, double avg_seg_bytes) {
 }
 
 // ---- two-pass tile kernel setup (gh_mtile.hip) -------------------------------------
-// Codes for it: complete, 2 <= len <= 12 (at most 64 codewords per segment), not taken
-// by the single-pass tile kernel.  One LUT of width K (the wave split's write width) with
-// the codewords' start masks; one staging region per wave, sized for the stream's mean
-// bytes per segment + 12 % and at least one chain's worst case (64 x 64 bytes: a larger
+// Codes for it: complete, 1 <= len <= 16 (at most 128 codewords per segment), not taken
+// by the single-pass tile kernel.  One LUT of width K (the wave split's write width; 11
+// with a 1-bit codeword) with the codewords' start masks; one staging region per wave, sized for the stream's mean
+// bytes per segment + 12 % and at least one chain's worst case (64 x 128 / minlen bytes: a larger
 // piece is written and copied out chain by chain).  Returns GH_OK with c->tile false when
 // it does not fit a CU.
 static uint32_t ws_write_bits(const Canon& cn);
 static int mtile_setup(gh_ctx* c, double avg_seg_bytes) {
   const Canon& cn = c->canon;
-  const uint32_t K = ws_write_bits(cn);
+  // codes with a 1-bit codeword: segments of up to 128 codewords, a chain's worst case
+  // 8 KB, so 11-bit tables (24 KB with the count table) leave 16 regions of 8.5 KB
+  const bool one = cn.minlen == 1;
+  const uint32_t K = one ? std::min<uint32_t>(ws_write_bits(cn), 11) : ws_write_bits(cn);
   // codewords longer than the tables (up to 16 bits) take the canonical fallback, with
   // two lookups per window shift (2 x 12 + 16 > 32 otherwise)
   const bool fb = K < cn.maxlen;
-  if (fb && (K != 12 || cn.maxlen > 16)) return GH_OK;
-  const uint32_t maxsyms = (128 + cn.minlen - 1) / cn.minlen;  // <= 64
+  // (and windows that reach a 16-bit codeword's last bit: K = 12, or 11 in the kernels
+  // for codes with a 1-bit codeword, gh_mtile.hip)
+  if (fb && (K != (one ? 11u : 12u) || cn.maxlen > 16)) return GH_OK;
+  const uint32_t maxsyms = (128 + cn.minlen - 1) / cn.minlen;  // <= 128
   double scapf = 1.12;
   if (const char* e = getenv("GH_TILE_SCAPF")) scapf = std::clamp(atof(e), 0.5, 4.0);
   uint64_t per_seg = std::min<uint64_t>(maxsyms, (uint64_t)std::ceil(std::max(avg_seg_bytes, 1.0) * scapf + 1));
@@ -292,7 +298,7 @@ static int mtile_setup(gh_ctx* c, double avg_seg_bytes) {
   // count table width: wider than the write table's (more codewords per lookup) where
   // the LDS and a window shift allow it (GL lookups of Kc bits within 31 bits)
   uint32_t Kc = K;
-  if (GH_MT_CLUT) {
+  if (GH_MT_CLUT && !one) {
     const int gl = lookups_per_shift(K);
     Kc = std::min<uint32_t>(13, 31 / gl);
     if (const char* e = getenv("GH_MT_KC")) Kc = (uint32_t)std::clamp(atoi(e), (int)K, (int)std::min(14, 31 / gl));
@@ -302,7 +308,8 @@ static int mtile_setup(gh_ctx* c, double avg_seg_bytes) {
   const uint64_t lut_b = (GH_MT_CLUT ? (8ull << K) + (4ull << Kc) : 8ull << K)  // write table (+ count table)
                          + (fb ? (uint64_t)FB_BYTES : 0);                         // (+ fallback tables)
   const uint64_t lds_free = 160ull * 1024 - lut_b - mtile_lds_bytes(0, 0);
-  const uint64_t region_max = std::min<uint64_t>(lds_free / (MT_TB / 64), 8 * 1024 + STAGE_PAD) & ~15ull;
+  // (the copy-out: 8 x 64 chunks, or 2 x 5 x 64 for codes with a 1-bit codeword)
+  const uint64_t region_max = std::min<uint64_t>(lds_free / (MT_TB / 64), (one ? 10 : 8) * 1024 + STAGE_PAD) & ~15ull;
   per_seg = std::min<uint64_t>(per_seg, (region_max - STAGE_PAD - 16) / (64ull * MT_U));
   {  // six copy-out stores per lane (the 8-store kernel spills at lag 3) when the mean + 5 % fits
     const uint64_t ps6 = (6144 - 16) / (64ull * MT_U);
@@ -310,7 +317,7 @@ static int mtile_setup(gh_ctx* c, double avg_seg_bytes) {
   }
   const uint64_t cap = std::max<uint64_t>(64ull * MT_U * per_seg, 64ull * maxsyms);  // piece bytes staged at once
   if (STAGE_PAD + cap + 16 > region_max) return GH_OK;
-  c->mt_ns = cap + 16 <= 4096 ? 4 : cap + 16 <= 6144 ? 6 : 8;  // the copy-out's chunks cover a piece
+  c->mt_ns = cap + 16 <= 4096 ? 4 : cap + 16 <= 6144 ? 6 : cap + 16 <= 8192 ? 8 : 10;  // the copy-out's chunks cover a piece
   c->stage_bytes = (uint32_t)((STAGE_PAD + cap + 16 + 15) & ~15ull);  // + the write overrun
   c->mt_gl = lookups_per_shift(K);
   c->mt_fb = fb;
@@ -546,7 +553,7 @@ extern "C" int gh_ctx_create(int device, gh_ctx** out) {
     for (uint32_t gv : {2u, 3u, 4u})
       (void)hipFuncSetAttribute(tile_kernel_for(ml, gv), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   for (int gl : {2, 3, 4})
-    for (int ns : {4, 6, 8})
+    for (int ns : {4, 6, 8, 10})
       for (bool fb : {false, true})
         (void)hipFuncSetAttribute(mtile_kernel_for(gl, ns, fb), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   (void)hipGetLastError();
@@ -656,9 +663,9 @@ static int load_common(gh_ctx* c, const gh_stream* s, uint64_t b, uint64_t e, ui
     // the two-pass tile kernel: codes of 2..12-bit codewords the single-pass one does not
     // take (cfg3's r = 0.9 codes; GH_MTILE=0 leaves them to the wave split, GH_MODE=mtile
     // forces it)
-    const bool multi = cn.minlen >= 2 && cn.maxlen <= 16 && kraft16(cn) == 65536;
+    const bool multi = cn.maxlen <= 16 && kraft16(cn) == 65536;
     if (force_mt && !multi)
-      return fail(GH_E_ARG, "GH_MODE=mtile: the code is not for the two-pass tile kernel (complete, 2..16 bits)");
+      return fail(GH_E_ARG, "GH_MODE=mtile: the code is not for the two-pass tile kernel (complete, 1..16 bits)");
     static const bool mt_on = [] {
       const char* e = getenv("GH_MTILE");
       return !(e && e[0] == '0');

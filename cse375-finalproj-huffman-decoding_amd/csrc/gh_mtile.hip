@@ -1,12 +1,14 @@
-// Two-pass tile kernel: the decode of short-codeword codes (complete, 2 <= len <= 12,
-// multi-symbol lookups worth >= 1.5 codewords, e.g. BASELINE's r = 0.9 data), included by
+// Two-pass tile kernel: the decode of short-codeword codes (complete, 1 <= len <= 16,
+// multi-symbol lookups worth >= 1.5 codewords, e.g. BASELINE's r = 0.9 data; codewords
+// longer than the tables through a canonical fallback), included by
 // gh_decode.hip after gh_tile.hip (whose round leader, prefix granules, copy-out and LDS
 // helpers it shares).  Reference counterpart: gpu_dec_l1_l2 (decoder/src/decoder.cu:
 // 454-730) — its count pass (:529-569), decoupled look-back (:571-653) and decode pass
 // (:655-728) — with the payload read from HBM ONCE: the two passes run over the same
 // register-resident words, one tile apart.
 //
-// A segment of these codes holds up to 64 codewords, too many to keep as bytes in
+// A segment of these codes holds up to 64 codewords (128 with a 1-bit codeword: 11-bit
+// tables then, 8.5 KB regions, and a copy-out in two parts, NP = 2), too many to keep as bytes in
 // registers (the single-pass tile kernel's way), so a tile is decoded twice from its
 // words, with one table of up to four codewords per lookup,
 //   entry = {symbols (bytes 0..3), b | n << 8 | startmask << 16}
@@ -66,7 +68,8 @@ constexpr int MT_LAG = GH_MT_LAG;
 #ifndef GH_MT_NOFB
 #define GH_MT_NOFB 0  // experiment: no chain-by-chain path
 #endif
-constexpr int MT_GMAX = 80;         // lookup groups per segment, at most (>= 2 bits per lookup)
+constexpr int MT_GMAX = 80;         // lookup groups per segment, at most (>= 1 codeword and >= 1 bit per lookup,
+                                    // GL = 2: <= 64 groups to cover 128 codewords / bits)
 
 // Advance a 5-word e-window by 32 - (q & 31) bits.
 __device__ __forceinline__ void win_shift5(uint32_t (&e)[5], uint32_t q) {
@@ -100,7 +103,7 @@ inline size_t mtile_lds_bytes(size_t lut_bytes, size_t stage_bytes) {
 // Count pass of U segments per lane on e-windows (S = 29 - K, u64 entries): codewords
 // that start before the segment end, R = 128 - start bits away.  GL lookups per window
 // shift (GL * K <= 24 bits: rm, recomputed per group from R, covers the group's starts).
-template <int U, int GL, bool FB = false>
+template <int U, int GL, bool FB = false, int SH = 0>
 __device__ __forceinline__ void mt_count(uint32_t (&e)[U][5], const int (&R0)[U], uint32_t (&cnt)[U], uint32_t amask,
                                          uint32_t cbase, const MtFb& fb = MtFb{}, uint32_t Sc = 0) {
   int R[U];
@@ -122,7 +125,7 @@ __device__ __forceinline__ void mt_count(uint32_t (&e)[U][5], const int (&R0)[U]
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const uint32_t x = j == 0 ? e[u][0] : __builtin_amdgcn_alignbit(e[u][0], e[u][1], q[u]);
-        hi[u] = lds_u32_nowait((x & amask) | cbase);  // the count entry (or the write entry's high word)
+        hi[u] = lds_u32_nowait(((x >> SH) & amask) | cbase);  // the count entry (or the write entry's high word)
       }
       lds_wait(hi);
       if constexpr (FB) {
@@ -158,7 +161,7 @@ __device__ __forceinline__ void mt_count(uint32_t (&e)[U][5], const int (&R0)[U]
 
 // Write pass: the n[u] codewords of each segment to LDS bytes [o[u], o[u] + n[u]) (then
 // the head stores, above).  A chain with n = 0 writes nothing.
-template <int U, int GL, bool FB = false>
+template <int U, int GL, bool FB = false, int SH = 0>
 __device__ __forceinline__ void mt_write(uint32_t (&e)[U][5], const uint32_t (&o)[U], const uint32_t (&n)[U],
                                          uint32_t amask, uint32_t wbase, const MtFb& fb = MtFb{}, uint32_t Sw = 0) {
   uint32_t ptr[U], end[U], head[U];
@@ -186,7 +189,7 @@ __device__ __forceinline__ void mt_write(uint32_t (&e)[U][5], const uint32_t (&o
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const uint32_t x = j == 0 ? e[u][0] : __builtin_amdgcn_alignbit(e[u][0], e[u][1], q[u]);
-        ent[u] = lds_u64_nowait((x & amask) | wbase);
+        ent[u] = lds_u64_nowait(((x >> SH) & amask) | wbase);
       }
       lds_wait(ent);
       if constexpr (FB) {
@@ -278,7 +281,7 @@ __device__ __forceinline__ void mt_zero(uint32_t region, uint32_t n, int lane) {
     asm volatile("ds_write_b128 %0, %1" ::"v"(region + 16u * c), "v"(tile_v4u{0, 0, 0, 0}) : "memory");
 }
 
-template <int TB, int GL, int NS, bool FB = false>
+template <int TB, int GL, int NS, bool FB = false, int NP = 1>
 __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void gh_mtile_kernel(const TileParams p) {
   constexpr int U = MT_U;
   constexpr int NW = TB / 64;
@@ -308,13 +311,17 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
       s_ptile[tid] = 0xFFFFFFFFu;
     }
   }
-  const uint32_t S = 29u - p.kbits;                        // write pass: u64 entries
+  // (FB, NP = 2: 11-bit tables on windows of S = 17, the lookups shifted down: a window
+  // holds segment bits start - S .. start - S + 159, and a 16-bit codeword at bit 127
+  // ends at bit 142, so S <= 17 for the fallback to see all its bits)
+  constexpr int WSH = (FB && NP == 2) ? 1 : 0, CSH = (FB && NP == 2) ? 2 : 0;
+  const uint32_t S = 29u - p.kbits - WSH;                  // write pass: u64 entries
   const uint32_t amask = ((1u << p.kbits) - 1u) << 3;
   // count pass: its own u32 table of width Kc (GH_MT_CLUT), the larger of the two
   // tables first so that each base ORs into its table's addresses; or the write table's
   // high words
   const uint32_t Kc = GH_MT_CLUT ? p.kbits_c : p.kbits;
-  const uint32_t Sc = GH_MT_CLUT ? 30u - Kc : S;
+  const uint32_t Sc = GH_MT_CLUT ? 30u - Kc - CSH : S;
   const uint32_t amask_c = GH_MT_CLUT ? ((1u << Kc) - 1u) << 2 : amask;
   const bool cfirst = GH_MT_CLUT && (4u << Kc) > (8u << p.kbits);
   const uint32_t cbase = !GH_MT_CLUT ? 4u : cfirst ? 0u : 8u << p.kbits;
@@ -348,8 +355,9 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
   {  // as many stores after these loads as every iteration issues after its prefetch
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(p.out, 0, 0x7FFFFFF0, 0x00020000);
 #pragma unroll
-    for (int i = 0; i < NS; ++i) __builtin_amdgcn_raw_buffer_store_b128(tile_v4u{0, 0, 0, 0}, rs, (int)(OOB_OFF + 16u * (uint32_t)i), 0, 2);  // (distinct: not merged)
-    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)0, rs, (int)OOB_OFF, 0, 2);
+    for (int i = 0; i < NS * NP; ++i) __builtin_amdgcn_raw_buffer_store_b128(tile_v4u{0, 0, 0, 0}, rs, (int)(OOB_OFF + 16u * (uint32_t)i), 0, 2);  // (distinct: not merged)
+#pragma unroll
+    for (int i = 0; i < NP; ++i) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)0, rs, (int)(OOB_OFF + 16u * (uint32_t)i), 0, 2);
   }
   if (cur >= p.ntiles) cur = NONE;
   // tiles k-1 .. k-LAG, held for their write pass: e-windows, the segments' offsets in
@@ -413,7 +421,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
 #pragma unroll
         for (int u = 0; u < U; ++u) cnt[u] = R[u] > 0 ? 40u : 0u;
       } else {
-        mt_count<U, GL, FB>(e, R, cnt, amask_c, cbase, fb, Sc);
+        mt_count<U, GL, FB, CSH>(e, R, cnt, amask_c, cbase, fb, Sc);
       }
     }
     const unsigned long long gp = __hip_atomic_load(pf2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -457,7 +465,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
       uint32_t o[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) o[u] = region + STAGE_PAD + hpos[L - 1][u];
-      mt_write<U, GL, FB>(he[L - 1], o, hcnt[L - 1], amask, wbase, fb, S);
+      mt_write<U, GL, FB, WSH>(he[L - 1], o, hcnt[L - 1], amask, wbase, fb, S);
     }
     // ---- the prefix of tile k-1 -> this wave's piece's output offset (gh_tile.hip) --------
     unsigned long long goff = 0;
@@ -510,9 +518,12 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     }
     // ---- copy-out ---------------------------------------------------------------------------
     if (fits) {
-      tile_v4u cv[NS];
-      uint32_t cb;
-      copy_out_piece<NS, false>(p.out, region, goff, n2, lane, cv, cb);  // fixed store count (n2 = 0: all dropped)
+#pragma unroll
+      for (int part = 0; part < NP; ++part) {  // (NP parts of 64 * NS chunks: pieces of up to 8 KB)
+        tile_v4u cv[NS];
+        uint32_t cb;
+        copy_out_piece<NS, false>(p.out, region, goff, n2, lane, cv, cb, 64u * NS * (uint32_t)part);  // fixed store count
+      }
       if (GH_MT_WOR) mt_zero(region, wtot, lane);
     } else {
       // a piece larger than the region (data whose shortest codewords cluster): one chain
@@ -535,12 +546,15 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
         for (int v = 0; v < U; ++v)
 #pragma unroll
           for (int i = 0; i < 5; ++i) ew[v][i] = he[L - 1][v][i];
-        mt_write<U, GL, FB>(ew, o, nn, amask, wbase, fb, S);
+        mt_write<U, GL, FB, WSH>(ew, o, nn, amask, wbase, fb, S);
         const unsigned long long gu = goff + c0;
         const uint32_t nu = (!got || gu >= p.out_cap) ? 0u : (uint32_t)min<unsigned long long>(ct, p.out_cap - gu);
-        tile_v4u cv[NS];
-        uint32_t cb;
-        copy_out_piece<NS, false>(p.out, region, gu, nu, lane, cv, cb);
+#pragma unroll
+        for (int part = 0; part < NP; ++part) {
+          tile_v4u cv[NS];
+          uint32_t cb;
+          copy_out_piece<NS, false>(p.out, region, gu, nu, lane, cv, cb, 64u * NS * (uint32_t)part);
+        }
         if (GH_MT_WOR) mt_zero(region, ct, lane);
       }
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)

@@ -433,7 +433,9 @@ constexpr uint32_t OOB_OFF = 0x80000000u;  // a buffer offset past every range: 
 // right after the copy-out stalled the next iteration on the stores.
 template <int NS, bool PIN = true>
 __device__ __forceinline__ void copy_out_piece(uint8_t* out, uint32_t stg, unsigned long long goff, uint32_t n,
-                                               int lane, tile_v4u (&v)[NS], uint32_t& b) {
+                                               int lane, tile_v4u (&v)[NS], uint32_t& b, uint32_t c0 = 0) {
+  // (c0: the first chunk of this call; a piece copied in parts, 64 * NS chunks each, has
+  // its edge bytes stored by the part with c0 = 0)
   // goff and n are wave-uniform; said so explicitly, the buffer resource lives in SGPRs
   // (otherwise each store became a readfirstlane "waterfall" loop, and the compiler's
   // vmcnt counting across those loops fell back to short counts at the next iteration)
@@ -447,7 +449,7 @@ __device__ __forceinline__ void copy_out_piece(uint8_t* out, uint32_t stg, unsig
   uint32_t off[NS];
 #pragma unroll
   for (int i = 0; i < NS; ++i) {
-    const uint32_t c = cf + (uint32_t)lane + 64u * (uint32_t)i;
+    const uint32_t c = c0 + cf + (uint32_t)lane + 64u * (uint32_t)i;
     off[i] = c < ce ? 16u * c : OOB_OFF;
     if (PIN) asm volatile("ds_read_b128 %0, %1" : "+v"(v[i]) : "v"(src + 16u * (c < ce ? c : cf)) : "memory");
     else asm volatile("ds_read_b128 %0, %1" : "=v"(v[i]) : "v"(src + 16u * (c < ce ? c : cf)) : "memory");
@@ -459,8 +461,10 @@ __device__ __forceinline__ void copy_out_piece(uint8_t* out, uint32_t stg, unsig
   const uint32_t nt = (n && tl && (ce > 0 || !lb)) ? tl : 0u;
   const uint32_t t = (uint32_t)lane;
   uint32_t k = OOB_OFF;
-  if (t < nh) k = lb + t;
-  else if (t < nh + nt) k = 16u * ce + (t - nh);
+  if (c0 == 0u) {
+    if (t < nh) k = lb + t;
+    else if (t < nh + nt) k = 16u * ce + (t - nh);
+  }
   if (PIN) asm volatile("ds_read_u8 %0, %1" : "+v"(b) : "v"(src + (k == OOB_OFF ? 0u : k)) : "memory");
   else asm volatile("ds_read_u8 %0, %1" : "=v"(b) : "v"(src + (k == OOB_OFF ? 0u : k)) : "memory");
   asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b)::"memory");

@@ -1,6 +1,6 @@
 """GPU parity tests of the two-pass tile kernel (gh_mtile.hip, GH_MODE=mtile): complete
-codes of 2..16-bit codewords (those above 12 bits through a canonical fallback; BASELINE's r = 0.9 codes, and the r = 0.5 / 0.1 codes too
-when forced) decoded by one persistent kernel that reads the payload once: a count pass
+codes of 1..16-bit codewords (those above the 11- or 12-bit tables through a canonical fallback; BASELINE's
+r = 0.9 codes, and the r = 0.5 / 0.1 codes too when forced) decoded by one persistent kernel that reads the payload once: a count pass
 and, one tile later, a write pass over the same register-resident words.  Bit-exact
 against the CPU oracle and the original input (reference: decoder/src/decoder.cu:454-730,
 restated in oracle/gh_oracle.c)."""
@@ -37,8 +37,8 @@ def _complete(syms):
     return sum(2.0 ** -l for _, l in syms) == 1.0
 
 
-def _takes(syms):  # the kernel's codes: complete, codewords of 2..16 bits (> 12 through its fallback)
-    return _complete(syms) and max(l for _, l in syms) <= 16 and min(l for _, l in syms) >= 2
+def _takes(syms):  # the kernel's codes: complete, codewords of 1..16 bits (longer than the tables: fallback)
+    return _complete(syms) and max(l for _, l in syms) <= 16
 
 
 @pytest.mark.parametrize("r", [0.1, 0.5, 0.9, 0.999])
@@ -59,8 +59,9 @@ def test_mtile_vs_oracle(gpu, orc, mtile, r, n):
 
 
 def test_mtile_small_codes(gpu, orc, mtile):
-    # two-bit codes (four symbols: 64 codewords per segment, the most), 8-bit codes and a
-    # segment-multiple stream; one-bit codes are refused (the wave split takes them)
+    # two-bit codes (four symbols: 64 codewords per segment), 8-bit codes, a
+    # segment-multiple stream, one-bit codes (128 codewords per segment, the most) and a
+    # code whose 1-bit codeword takes 97 % of the stream
     rng = np.random.default_rng(3)
     four = (rng.integers(0, 4, 300_001) + 48).astype(np.uint8)
     assert {l for _, l in gpu.parse(gpu.encode(four)).symbols} == {2}
@@ -68,35 +69,50 @@ def test_mtile_small_codes(gpu, orc, mtile):
     data = np.tile(np.arange(256, dtype=np.uint8), 64)
     rng.shuffle(data)
     _check(gpu, orc, data)
-    two = (rng.integers(0, 2, 3001) + 48).astype(np.uint8)
-    with pytest.raises(gpu.GapHuffError):
-        gpu.decode(gpu.encode(two))
+    for n in (3001, 1_000_003):
+        two = (rng.integers(0, 2, n) + 48).astype(np.uint8)
+        img = _check(gpu, orc, two)
+        assert {l for _, l in gpu.parse(img).symbols} == {1}
+        assert gpu.MODE_NAMES[_report(gpu, img).mode] == "mtile"
+    skew = np.where(rng.random(2_000_003) < 0.97, 7, rng.integers(0, 256, 2_000_003)).astype(np.uint8)
+    img = _check(gpu, orc, skew)
+    assert min(l for _, l in gpu.parse(img).symbols) == 1
 
 
-@pytest.mark.parametrize("q,n", [(0.7, 300_001), (0.7, 3_000_017), (0.75, 1_000_003)])
+@pytest.mark.parametrize("q,n", [(0.7, 300_001), (0.7, 3_000_017), (0.75, 1_000_003), (0.5, 300_001),
+                                 (0.5, 3_000_017), (0.6, 1_000_003)])
 def test_mtile_long_codes_fallback(gpu, orc, monkeypatch, q, n):
-    """Codes of 2..16-bit codewords (geometric byte distributions): the codewords longer
-    than the 12-bit tables go through the canonical fallback inside the kernel; the
-    launcher picks the two-pass kernel for them by default."""
+    """Codes of 1..16-bit codewords (geometric byte distributions): the codewords longer
+    than the tables (12 bits; 11 for codes with a 1-bit codeword) go through the canonical
+    fallback inside the kernel; the launcher picks the two-pass kernel for them by default."""
     rng = np.random.default_rng(int(q * 100) + n)
     p = q ** np.arange(256, dtype=np.float64)
     p /= p.sum()
     data = rng.choice(256, size=n, p=p).astype(np.uint8)
     img = gpu.encode(data)
     lens = [l for _, l in gpu.parse(img).symbols]
-    assert min(lens) >= 2 and max(lens) > 12
+    assert min(lens) == (1 if q <= 0.6 else 2) and max(lens) > 12
     _check(gpu, orc, data)
     rep = _report(gpu, img)
     assert gpu.MODE_NAMES[rep.mode] == "mtile" and rep.status == 0
 
 
-def test_mtile_refuses_fallback_codes(gpu, mtile):
-    """Codes with a 1-bit codeword (here also 16-bit ones) stay with the wave split:
-    GH_MODE=mtile fails loudly at load."""
+def test_mtile_one_to_sixteen_bits(gpu, orc, mtile):
+    """A code of 1..16-bit codewords (a 1-bit one and 16-bit ones), sorted runs: segments
+    of 128 one-bit codewords first (their pieces go chain by chain), then long ones."""
     counts = [max(1, int(2 ** (24 - 0.9 * i))) for i in range(40)]
     data = np.repeat(np.arange(40, dtype=np.uint8), counts)
-    s = gpu.parse(gpu.encode(data))
+    img = _check(gpu, orc, data)
+    s = gpu.parse(img)
     assert min(l for _, l in s.symbols) == 1 and max(l for _, l in s.symbols) == 16
+    assert gpu.MODE_NAMES[_report(gpu, img).mode] == "mtile"
+
+
+def test_mtile_refuses_incomplete_codes(gpu, mtile):
+    """An incomplete code (a one-symbol input's) stays with the wave split: GH_MODE=mtile
+    fails loudly at load."""
+    s = gpu.parse(gpu.encode(np.full(1000, 5, np.uint8)))
+    assert not _complete(s.symbols)
     with gpu.Decoder(0) as d:
         with pytest.raises(gpu.GapHuffError):
             d.load(s)
@@ -119,6 +135,42 @@ def test_mtile_staging_overflow(gpu, orc, mtile, r, scap, monkeypatch):
         img = _check(gpu, orc, x)
         rep = _report(gpu, img)
         assert gpu.MODE_NAMES[rep.mode] == "mtile" and rep.status == 0
+
+
+def _geometric(q, n, seed):
+    rng = np.random.default_rng(seed)
+    p = q ** np.arange(256, dtype=np.float64)
+    p /= p.sum()
+    return rng.choice(256, size=n, p=p).astype(np.uint8)
+
+
+@pytest.mark.parametrize("scap", [None, "66", "40", "4"])
+def test_mtile_one_bit_staging(gpu, orc, mtile, scap, monkeypatch):
+    """Codes with a 1-bit codeword (q = 0.5: 64 codewords per segment on average, 128 at
+    most): 8.5 KB regions hold the mean piece of 8 KB, a chain's worst case (8 KB) is
+    copied out in two parts; sorted data and smaller caps take the chain-by-chain path."""
+    if scap:
+        monkeypatch.setenv("GH_TILE_SCAP", scap)
+    d = _geometric(0.5, 2_000_003, 41)
+    dense = np.sort(d)  # symbol 0 (the 1-bit codeword) first
+    for x in (dense, d):
+        img = _check(gpu, orc, x)
+        assert min(l for _, l in gpu.parse(img).symbols) == 1
+        rep = _report(gpu, img)
+        assert gpu.MODE_NAMES[rep.mode] == "mtile" and rep.status == 0
+
+
+def test_mtile_one_bit_capacity_and_shards(gpu, orc, mtile):
+    data = _geometric(0.5, 1_500_007, 43)
+    s = gpu.parse(gpu.encode(data))
+    for cap in (1, 15, 8193, 777_777, 1_500_000):
+        with gpu.Decoder(0) as d:
+            d.load(s, 0, s.g, out_cap=cap)
+            d.decode()
+            rep = d.report()
+            assert rep.status == 0 and rep.out_bytes == cap
+            assert np.array_equal(d.download(cap), data[:cap])
+    _check(gpu, orc, data, ngpus=3, devices=[0] * 3)
 
 
 @pytest.mark.parametrize("r,scap", [(0.9, None), (0.9, "4"), (0.5, None)])
@@ -190,4 +242,9 @@ def test_mtile_corrupted_stream_terminates(gpu, mtile):
 @pytest.mark.parametrize("r", [0.9, 0.5])
 def test_mtile_100MB(gpu, mtile, r):
     data = gpu.generate(375, r, 10**8)
+    assert np.array_equal(gpu.decode(gpu.encode(data)), data)
+
+
+def test_mtile_100MB_one_bit(gpu, mtile):
+    data = _geometric(0.5, 10**8, 377)
     assert np.array_equal(gpu.decode(gpu.encode(data)), data)
