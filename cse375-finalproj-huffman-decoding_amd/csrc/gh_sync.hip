@@ -49,6 +49,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -62,11 +64,12 @@ namespace {
 constexpr int SK = 13;          // LUT prefix bits (12: cfg4 2.28 ms, 13: 2.08, 14: 3.10 - occupancy)
 constexpr int SYNC_TB = 256;    // threads per workgroup
 #ifndef GH_SYNC_M
-#define GH_SYNC_M 16
+#define GH_SYNC_M 32  // (round 5: 32 with the code's own halo; 16 with 6 warm-up segments: cfg4 1.05 ms)
 #endif
 constexpr uint32_t SYNC_M = GH_SYNC_M;  // segments per lane (a multiple of 8: whole gap words)
 static_assert(SYNC_M % 8 == 0, "a lane writes whole gap words");
-constexpr int SYNC_HALO = 6;          // warm-up segments per lane (GH_SYNC_HALO overrides)
+// warm-up segments per lane: from the stream's resynchronisation distances (sync_halo_for;
+// GH_SYNC_HALO overrides)
 
 #define GH_HIPS(expr)                                                             \
   do {                                                                            \
@@ -418,6 +421,68 @@ void build_sync_tables(const Canon& c, SyncTables& st) {
   }
 }
 
+// Warm-up segments for a stream.  Walks from arbitrary bits resynchronise after a
+// distance that depends on the code and the data (simulated on the oracle: r = 0.9
+// codes 10 bits on average, r = 0.1 117, r = 0.5 326 with a p99 of 2390), and a block
+// whose walk has not merged with the true path by its first boundary costs its whole
+// wave a lock-step re-walk.  So the halo h minimises (M + h) + 64 * P(d > 128 h) * M / 2
+// (the walk, plus the chance that one of a wave's 64 blocks is re-walked, about half a
+// block), with P from the stream itself: its first words (a true codeword start at bit
+// 0) decoded from the start, then walked from 4096 pseudo-random bit offsets with the
+// kernels' rule (length 1 outside the code space) until a walk stands on a true start.
+// A short stream (few waves per SIMD: one wave's repair rounds then extend the whole
+// kernel) takes at least the p99.9 distance + 1 segment (cfg2: p99.9 ~4300 bits; h = 32
+// 0.144 ms, 20 0.168, 43-48 0.169-0.178).  In [2, 48].  `sample`: the stream's first words (zero padded by 2).
+uint32_t sync_halo_for(const SyncTables& st, const std::vector<uint32_t>& sample, uint64_t nbits, bool short_stream) {
+  if (nbits < 4096) return 2;
+  auto p16_at = [&](uint64_t pos) {
+    const uint64_t w = ((uint64_t)sample[pos >> 5] << 32) | sample[(pos >> 5) + 1];
+    return (uint32_t)((w << (pos & 31)) >> 48);
+  };
+  auto len_at = [&](uint64_t pos) {
+    const uint32_t p16 = p16_at(pos);
+    const uint32_t l = (st.lut[p16 >> (16 - SK)] >> 5) & 31u;
+    if (l) return l;
+    for (uint32_t m = SK + 1; m <= GH_MAX_CODE_LEN; ++m)
+      if (p16 < st.T[m]) return m;
+    return 1u;  // outside the code space
+  };
+  const uint64_t nb = nbits - 32;
+  std::vector<uint8_t> start(nb + 1, 0);
+  for (uint64_t pos = 0; pos < nb; pos += len_at(pos)) start[pos] = 1;
+  uint64_t x = 0x9E3779B97F4A7C15ull;
+  constexpr uint32_t NW = 4096, HMAX = 48;
+  std::vector<uint32_t> over(HMAX + 2, 0);  // walks not merged after h segments
+  std::vector<uint64_t> ds(NW);
+  for (uint32_t k = 0; k < NW; ++k) {
+    x ^= x << 13;
+    x ^= x >> 7;
+    x ^= x << 17;
+    const uint64_t o = x % (nb / 2);
+    uint64_t pos = o;
+    while (pos < nb && !start[pos]) pos += len_at(pos);
+    const uint64_t d = pos < nb ? pos - o : ~0ull;
+    ds[k] = d;
+    for (uint32_t h = 0; h <= HMAX; ++h)
+      if (d > 128ull * h) ++over[h];
+  }
+  uint32_t best = 2;
+  double best_c = 1e30;
+  for (uint32_t h = 2; h <= HMAX; ++h) {
+    const double c = (double)(SYNC_M + h) + 64.0 * ((double)over[h] / NW) * SYNC_M / 2;
+    if (c < best_c) {
+      best_c = c;
+      best = h;
+    }
+  }
+  if (short_stream) {
+    std::sort(ds.begin(), ds.end());
+    const uint64_t p999 = ds[NW - 1 - NW / 1000];
+    best = std::max<uint32_t>(best, (uint32_t)std::min<uint64_t>(HMAX, (p999 + 127) / 128 + 1));
+  }
+  return best;
+}
+
 struct DevBuf {
   void* p = nullptr;
   ~DevBuf() { (void)hipFree(p); }
@@ -473,8 +538,19 @@ extern "C" int gh_sync_gaps(int device, const gh_sym* syms, uint32_t nsyms, cons
   p.counter = (unsigned int*)counter.p;
   {
     const char* eh = getenv("GH_SYNC_HALO");
-    const int h = eh ? atoi(eh) : SYNC_HALO;
-    p.halo = (uint32_t)std::clamp(h, 0, 64);
+    if (eh) {
+      p.halo = (uint32_t)std::clamp(atoi(eh), 0, 64);
+    } else {  // from the stream's first words (at most 64 KiB; before the timed region)
+      const uint64_t ns = std::min<uint64_t>(w, 16384);
+      std::vector<uint32_t> sample(ns + 2, 0);
+      GH_HIPS(hipMemcpyAsync(sample.data(), d_words, 4 * ns, hipMemcpyDeviceToHost, st));
+      GH_HIPS(hipStreamSynchronize(st));
+      int ncu = 256;
+      if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) ncu = 256;
+      const bool short_stream = ceil_div(nblk, (uint64_t)64) < 8ull * 4 * (uint64_t)ncu;  // < 8 waves per SIMD
+      p.halo = sync_halo_for(tabs, sample, 32 * ns, short_stream);
+    }
+    if (getenv("GH_SYNC_VERBOSE")) fprintf(stderr, "gh_sync: %u segments per lane, halo %u\n", SYNC_M, p.halo);
   }
   hipEvent_t e0, e1;
   GH_HIPS(hipEventCreate(&e0));

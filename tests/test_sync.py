@@ -216,10 +216,12 @@ def test_gpu_decode_raw_roundtrip(gpu, orc, r):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,stride", [(100_000, 0), (40_000, 997)])
-def test_gpu_sync_repairs_desync(gpu, orc, n, stride):
+def test_gpu_sync_repairs_desync(gpu, orc, n, stride, monkeypatch):
     """Adversarial code whose walks never resynchronise on their own: the in-wave
     verify and the fix pass must find the mismatches and the repairs must fix every
-    boundary (a stream of one wave's blocks needs no second fix pass)."""
+    boundary (a stream of one wave's blocks needs no second fix pass).  The halo is held
+    at 6 segments (the stream-derived one would avoid the mismatches this test needs)."""
+    monkeypatch.setenv("GH_SYNC_HALO", "6")
     syms = [(0, 1), (1, 3), (2, 3), (3, 3), (4, 3)]
     d = np.full(n, 4, dtype=np.uint8)
     if stride:
@@ -229,6 +231,9 @@ def test_gpu_sync_repairs_desync(gpu, orc, n, stride):
     assert rep.mismatches > 0 and rep.passes >= 1
     assert np.array_equal(gaps, orc.raw_gaps(d, syms))
     assert np.array_equal(gpu.decode_raw(units, syms, d.size), d)
+    monkeypatch.delenv("GH_SYNC_HALO")
+    gaps, rep = _sync_on_gpu(gpu, units, syms)  # the stream-derived halo: exact gaps too
+    assert np.array_equal(gaps, orc.raw_gaps(d, syms))
 
 
 @pytest.mark.gpu
