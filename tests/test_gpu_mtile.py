@@ -97,14 +97,17 @@ def test_mtile_long_codes_fallback(gpu, orc, monkeypatch, q, n):
     assert gpu.MODE_NAMES[rep.mode] == "mtile" and rep.status == 0
 
 
-def test_mtile_one_to_sixteen_bits(gpu, orc, mtile):
-    """A code of 1..16-bit codewords (a 1-bit one and 16-bit ones), sorted runs: segments
-    of 128 one-bit codewords first (their pieces go chain by chain), then long ones."""
-    counts = [max(1, int(2 ** (24 - 0.9 * i))) for i in range(40)]
-    data = np.repeat(np.arange(40, dtype=np.uint8), counts)
+@pytest.mark.parametrize("nsym,ratio,maxlen", [(40, 0.9, 16), (13, 1.0, 12), (12, 1.0, 11)])
+def test_mtile_one_to_sixteen_bits(gpu, orc, mtile, nsym, ratio, maxlen):
+    """Codes of 1..16-bit, 1..12-bit (one length past the 11-bit tables: the fallback)
+    and 1..11-bit codewords, sorted runs: segments of 128 one-bit codewords first (their
+    pieces go chain by chain), then long ones; and the same data shuffled."""
+    counts = [max(1, int(2 ** (24 - ratio * i))) for i in range(nsym)]
+    data = np.repeat(np.arange(nsym, dtype=np.uint8), counts)
     img = _check(gpu, orc, data)
     s = gpu.parse(img)
-    assert min(l for _, l in s.symbols) == 1 and max(l for _, l in s.symbols) == 16
+    assert min(l for _, l in s.symbols) == 1 and max(l for _, l in s.symbols) == maxlen
+    _check(gpu, orc, np.random.default_rng(nsym).permutation(data))
     assert gpu.MODE_NAMES[_report(gpu, img).mode] == "mtile"
 
 
