@@ -431,8 +431,8 @@ void build_sync_tables(const Canon& c, SyncTables& st) {
 // 0) decoded from the start, then walked from 4096 pseudo-random bit offsets with the
 // kernels' rule (length 1 outside the code space) until a walk stands on a true start.
 // A short stream (few waves per SIMD: one wave's repair rounds then extend the whole
-// kernel) takes at least the p99.9 distance + 1 segment (cfg2: p99.9 ~4300 bits; h = 32
-// 0.144 ms, 20 0.168, 43-48 0.169-0.178).  In [2, 48].  `sample`: the stream's first words (zero padded by 2).
+// kernel) takes at least the p99.9 distance, rounded up to segments (cfg2: p99.9 ~4300
+// bits; h = 32 0.144 ms, 35 0.154-0.156, 20 0.168, 43-48 0.169-0.178).  In [2, 48].  `sample`: the stream's first words (zero padded by 2).
 uint32_t sync_halo_for(const SyncTables& st, const std::vector<uint32_t>& sample, uint64_t nbits, bool short_stream) {
   if (nbits < 4096) return 2;
   auto p16_at = [&](uint64_t pos) {
@@ -478,7 +478,7 @@ uint32_t sync_halo_for(const SyncTables& st, const std::vector<uint32_t>& sample
   if (short_stream) {
     std::sort(ds.begin(), ds.end());
     const uint64_t p999 = ds[NW - 1 - NW / 1000];
-    best = std::max<uint32_t>(best, (uint32_t)std::min<uint64_t>(HMAX, (p999 + 127) / 128 + 1));
+    best = std::max<uint32_t>(best, (uint32_t)std::min<uint64_t>(HMAX, (p999 + 127) / 128));
   }
   return best;
 }
