@@ -237,6 +237,27 @@ def test_gpu_sync_repairs_desync(gpu, orc, n, stride, monkeypatch):
 
 
 @pytest.mark.gpu
+def test_gpu_sync_halo_follows_the_stream(gpu, orc, capfd, monkeypatch):
+    """The warm-up halo is chosen per stream from its sampled resynchronisation distances
+    (gh_sync.hip sync_halo_for): short for a fast-merging r = 0.9 code, long for r = 0.5
+    (slow merging, and a short stream), and the gaps stay exact either way."""
+    monkeypatch.setenv("GH_SYNC_VERBOSE", "1")
+    halos = {}
+    for r in (0.9, 0.5):
+        d = gpu.generate(11, r, 2_000_000)
+        s = gpu.parse(gpu.encode(d))
+        import ctypes
+        pw = np.ctypeslib.as_array(ctypes.cast(s.c.payload, ctypes.POINTER(ctypes.c_uint32)), (s.w,)).copy()
+        capfd.readouterr()
+        gaps, rep = _sync_on_gpu(gpu, pw, s.symbols)
+        err = capfd.readouterr().err
+        halos[r] = int(err.split("halo")[-1].split()[0])
+        gw = np.ctypeslib.as_array(ctypes.cast(s.c.gap_words, ctypes.POINTER(ctypes.c_uint32)), (gaps.size,))
+        assert np.array_equal(gaps, gw)
+    assert halos[0.9] <= 4 < 10 <= halos[0.5], halos
+
+
+@pytest.mark.gpu
 def test_gpu_decode_raw_empty(gpu):
     with gpu.Decoder(0) as dec:
         rep = dec.load_raw([(65, 1)], 0, np.zeros(0, np.uint32))
