@@ -261,7 +261,7 @@ static int tile_setup(gh_ctx* c, uint32_t K, double avg_seg_bytes) {
     }
   if (c->grid < 2) return GH_OK;  // (the wave split then takes the code)
   if (GH_TILE_STAMPS) {
-    const size_t nb = 32ull * c->grid * 2 * 128 + 8ull * (3ull * c->ntiles + 64 + 4 * 1024);
+    const size_t nb = 32ull * c->grid * 2 * 128 + 8ull * (3ull * c->ntiles + 64 + 4 * 1024 + 4ull * c->grid);
     GH_HIP(hipMalloc(&c->d_stamps, nb));
     GH_HIP(hipMemset(c->d_stamps, 0, nb));
   }
@@ -814,9 +814,11 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
       c->epoch = 1;
     }
     chain_lock.lock();
-    // (a decode on the same stream as the last one is ordered behind it already: no wait
-    // packet)
-    if (dc.has && dc.last_stream != st) GH_HIP(hipStreamWaitEvent(st, dc.last, 0));
+    // (the context's own stream, which the last tile decode of the device ran on for this
+    // same context, is ordered behind it already: no wait packet.  A caller's stream is
+    // never trusted that way: it may have been destroyed and its handle reused since.)
+    const bool ordered = dc.owner == c && dc.last_stream == st && st == c->stream;
+    if (dc.has && !ordered) GH_HIP(hipStreamWaitEvent(st, dc.last, 0));
   }
   std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
   if (timed) {
@@ -956,7 +958,7 @@ extern "C" int gh_ctx_report(gh_ctx* c, void* hip_stream, gh_report* rep) {
   c->pending.clear();
   if (GH_TILE_STAMPS && c->d_stamps) {  // diagnostic builds: the last decode's phase deltas
     if (const char* f = getenv("GH_STAMPS_OUT")) {
-      std::vector<uint8_t> h(32ull * c->grid * 2 * 128 + 8ull * (3ull * c->ntiles + 64 + 4 * 1024));
+      std::vector<uint8_t> h(32ull * c->grid * 2 * 128 + 8ull * (3ull * c->ntiles + 64 + 4 * 1024 + 4ull * c->grid));
       GH_HIP(hipMemcpy(h.data(), c->d_stamps, h.size(), hipMemcpyDeviceToHost));
       if (FILE* fp = fopen(f, "wb")) {
         fwrite(h.data(), 1, h.size(), fp);

@@ -49,6 +49,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -477,8 +478,8 @@ uint32_t sync_halo_for(const SyncTables& st, const std::vector<uint32_t>& sample
   }
   if (short_stream) {
     std::sort(ds.begin(), ds.end());
-    const uint64_t p999 = ds[NW - 1 - NW / 1000];
-    best = std::max<uint32_t>(best, (uint32_t)std::min<uint64_t>(HMAX, (p999 + 127) / 128));
+    const uint64_t p999 = ds[NW - 1 - NW / 1000];  // ~0 when 5 or more walks never merged
+    best = std::max<uint32_t>(best, p999 >= 128ull * HMAX ? HMAX : (uint32_t)((p999 + 127) / 128));
   }
   return best;
 }
@@ -536,8 +537,10 @@ extern "C" int gh_sync_gaps(int device, const gh_sym* syms, uint32_t nsyms, cons
   p.gaps = d_gap_words;
   p.check = (uint8_t*)check.p;
   p.counter = (unsigned int*)counter.p;
+  float host_ms = 0;
   {
     const char* eh = getenv("GH_SYNC_HALO");
+    const auto h0 = std::chrono::steady_clock::now();
     if (eh) {
       p.halo = (uint32_t)std::clamp(atoi(eh), 0, 64);
     } else {  // from the stream's first words (at most 64 KiB; before the timed region)
@@ -549,6 +552,7 @@ extern "C" int gh_sync_gaps(int device, const gh_sym* syms, uint32_t nsyms, cons
       if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) ncu = 256;
       const bool short_stream = ceil_div(nblk, (uint64_t)64) < 8ull * 4 * (uint64_t)ncu;  // < 8 waves per SIMD
       p.halo = sync_halo_for(tabs, sample, 32 * ns, short_stream);
+      host_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - h0).count();
     }
     if (getenv("GH_SYNC_VERBOSE")) fprintf(stderr, "gh_sync: %u segments per lane, halo %u\n", SYNC_M, p.halo);
   }
@@ -592,6 +596,8 @@ extern "C" int gh_sync_gaps(int device, const gh_sym* syms, uint32_t nsyms, cons
     rep->mismatches = mism;
     rep->passes = passes;
     rep->kernel_ms = ms;
+    rep->host_ms = host_ms;
+    rep->halo = p.halo;
   }
   return GH_OK;
 }

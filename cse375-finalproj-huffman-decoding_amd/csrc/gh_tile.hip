@@ -58,6 +58,18 @@ constexpr int TILE_SLOTS = 16;  // per-tile wave totals / offsets / arrival coun
 #else
 #define TSTAMP(i) ((void)0)
 #endif
+#ifndef GH_TILE_CSUB
+#define GH_TILE_CSUB 0  // the decode step's borrow count in C (the compiler's own hazard padding)
+#endif
+#ifndef GH_TILE_CLDS
+#define GH_TILE_CLDS 0  // the decode's LUT reads as plain LDS loads (the compiler's own lgkmcnt waits)
+#endif
+#ifndef GH_TILE_LMAJ
+#define GH_TILE_LMAJ 0  // lane-major segments: lane l of a wave decodes its segments U*l .. U*l + U - 1
+#endif
+#ifndef GH_TILE_POLLDIV
+#define GH_TILE_POLLDIV 1  // a waiting wave re-polls the prefix granule every N-th spin (staggered by wave)
+#endif
 #ifndef GH_TILE_ABLATE
 #define GH_TILE_ABLATE 0  // diagnostic builds only (make variant), bits: 1 no decode, 2 no staging
                           // stores, 4 no prefix wait (a fake offset), 8 no copy-out (wrong output)
@@ -140,6 +152,7 @@ __device__ __forceinline__ uint32_t q_init(bool act, int start) {
 template <int N>
 __device__ __forceinline__ void lds_wait_n(uint32_t& v) {
   static_assert(N >= 0 && N <= 3, "lgkmcnt 0..3");
+  if constexpr (GH_TILE_CLDS) return;  // (the compiler's own waits for plain LDS loads)
   if constexpr (N == 0) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v)::"memory");
   else if constexpr (N == 1) asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(v)::"memory");
   else if constexpr (N == 2) asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(v)::"memory");
@@ -170,6 +183,12 @@ __device__ __forceinline__ int decode_tile_rolling(uint32_t (&e)[U][5], const in
   constexpr int S = 4 * OW;
   constexpr int NG = (S + G - 1) / G;
   uint32_t q[U], ent[U];
+#if GH_TILE_CLDS
+  const __attribute__((address_space(3))) uint8_t* const lds0 = (const __attribute__((address_space(3))) uint8_t*)nullptr;
+  auto lut_rd = [&](uint32_t a) -> uint32_t { return *(const __attribute__((address_space(3))) uint32_t*)(lds0 + a); };
+#else
+  auto lut_rd = [&](uint32_t a) -> uint32_t { return lds_u32_nowait(a); };
+#endif
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     q[u] = q_init(act[u], start[u]);
@@ -178,7 +197,7 @@ __device__ __forceinline__ int decode_tile_rolling(uint32_t (&e)[U][5], const in
     for (int k = 0; k < OW; ++k) asm volatile("" : "=v"(ow[u][k]));
   }
 #pragma unroll
-  for (int u = 0; u < U; ++u) ent[u] = lds_u32_nowait((e[u][0] & amask) | laneoff);
+  for (int u = 0; u < U; ++u) ent[u] = lut_rd((e[u][0] & amask) | laneoff);
   int gdone = NG;
 #pragma clang loop unroll(full)
   for (int gi = 0; gi < NG; ++gi) {
@@ -207,13 +226,22 @@ __device__ __forceinline__ int decode_tile_rolling(uint32_t (&e)[U][5], const in
           } else {
             lds_wait_n<U - 1>(ent[u]);
           }
+#if GH_TILE_CSUB
+          {
+            uint32_t nq;
+            const bool br = __builtin_sub_overflow(q[u], ent[u], &nq);
+            q[u] = nq;
+            cnt[u] = br ? (uint32_t)(pos + 1) : cnt[u];
+          }
+#else
           asm("v_sub_co_u32 %0, vcc, %0, %2\n\t"
               "v_cndmask_b32_e64 %1, %1, %3, vcc"
               : "+v"(q[u]), "+v"(cnt[u]) : "v"(ent[u]), "i"(pos + 1) : "vcc");
+#endif
           ow[u][pos >> 2] = __builtin_amdgcn_perm(ent[u], ow[u][pos >> 2], perm_sel(pos & 3));
           if (!gend) {
             const uint32_t x = __builtin_amdgcn_alignbit(e[u][0], e[u][1], q[u]);
-            ent[u] = lds_u32_nowait((x & amask) | laneoff);
+            ent[u] = lut_rd((x & amask) | laneoff);
           } else {
             // window shift (the trim of words no kept codeword reads: above)
             e[u][0] = __builtin_amdgcn_alignbit(e[u][0], e[u][1], q[u]);
@@ -223,7 +251,7 @@ __device__ __forceinline__ int decode_tile_rolling(uint32_t (&e)[U][5], const in
             if (CMIN + 128 < 157) e[u][4] = __builtin_amdgcn_alignbit(e[u][4], 0u, q[u]);
             q[u] = (q[u] & 0xFFFFFF00u) | 32u;
             qmin = min(qmin, q[u]);
-            if (!last) ent[u] = lds_u32_nowait((e[u][0] & amask) | laneoff);
+            if (!last) ent[u] = lut_rd((e[u][0] & amask) | laneoff);
           }
         }
       }
@@ -535,6 +563,14 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     return;
   }
   if (blockIdx.x == p.idle_block) return;  // the leader's CU partner (GH_TILE_IDLE): no decoding
+#if GH_TILE_STAMPS
+  // per workgroup: shader-clock and 100 MHz times at its start and end (its clock)
+  unsigned long long* const wring = p.tstamps + 3ull * p.ntiles + 64 + 4ull * 1024 + 4ull * blockIdx.x;
+  if (tid == 0) {
+    wring[0] = __builtin_amdgcn_s_memtime();
+    wring[1] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
   {  // LUT to LDS, replicated: dword i of LDS = entry i >> lgr (lane l reads copy l mod 2^lgr,
      // so up to 32 lanes of a ds_read_b32 hit distinct banks)
     const uint32_t nd = p.lut_bytes >> 2;
@@ -556,18 +592,36 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
   __syncthreads();  // the LUT and the counters (the last barrier of a decoding workgroup)
   const uint32_t last_tile_k = b < p.ntiles ? (p.ntiles - 1 - b) / G : NONE;
   uint32_t cur = b, nxt = b + G;
-  // the lane's segments in a tile: wave-contiguous, 64 per chain
-  const uint32_t lseg = (uint32_t)(wid * 64 * U + lane);
+  // the lane's segments in a tile: wave-contiguous, 64 per chain (chain u lane l: segment
+  // 64u + l of the wave's 64U); lane-major (GH_TILE_LMAJ): lane l's U consecutive segments
+  // Ul .. Ul + U - 1, so the staging stores of one instruction land ~U segments apart
+  constexpr uint32_t CSTR = GH_TILE_LMAJ ? 1u : 64u;  // segment stride between chains
+  const uint32_t lseg = (uint32_t)(wid * 64 * U) + (uint32_t)lane * (GH_TILE_LMAJ ? (uint32_t)U : 1u);
   uint4 w[U];
   uint32_t w4[U], gw[U];
   auto load = [&](uint32_t t) {
     const uint32_t seg0 = min(t, p.ntiles - 1) * (uint32_t)(U * TB) + lseg;
+    if constexpr (GH_TILE_LMAJ) {
+      // one lane's U consecutive segments: their 16 U bytes and the next segment's first
+      // word (chain u's look-ahead word is chain u + 1's first word); past the shard end
+      // the lane reads the zero padding (inactive)
+      const uint32_t sb = min(seg0, nseg - 1);
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t sc = min(seg0 + (uint32_t)(64 * u), nseg - 1);
-      w[u] = *(const uint4*)(p.payload + 4ull * sc);
-      w4[u] = p.payload[4ull * sc + 4];
-      gw[u] = p.gaps[(p.gap_nib0 + (sc ? sc - 1u : 0u)) >> 3];
+      for (int u = 0; u < U; ++u) w[u] = *(const uint4*)(p.payload + 4ull * (sb + (uint32_t)u));
+      w4[U - 1] = p.payload[4ull * (sb + (uint32_t)U)];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t sc = sb + (uint32_t)u;
+        gw[u] = p.gaps[(p.gap_nib0 + (sc ? sc - 1u : 0u)) >> 3];
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t sc = min(seg0 + (uint32_t)(64 * u), nseg - 1);
+        w[u] = *(const uint4*)(p.payload + 4ull * sc);
+        w4[u] = p.payload[4ull * sc + 4];
+        gw[u] = p.gaps[(p.gap_nib0 + (sc ? sc - 1u : 0u)) >> 3];
+      }
     }
   };
   load(cur);
@@ -638,10 +692,10 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
       uint32_t e[U][5];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const uint32_t seg = seg0 + (uint32_t)(64 * u);
+        const uint32_t seg = seg0 + (uint32_t)u * CSTR;
         act[u] = have_cur && seg < nseg;
         start[u] = seg == 0 ? (int)p.first_start : (int)gap_nib(gw[u], p.gap_nib0 + seg - 1u);
-        make_ewin(w[u], w4[u], start[u], S, e[u]);
+        make_ewin(w[u], (GH_TILE_LMAJ && u + 1 < U) ? w[u + 1 < U ? u + 1 : u].x : w4[u], start[u], S, e[u]);
       }
       TSTAMP(1);
       if (GH_TILE_ABLATE & 1) {  // diagnostic build: no decode, 16 bytes per segment (wrong output)
@@ -667,13 +721,27 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     TSTAMP(2);
     // ---- wave scans: the segments' offsets in the wave's piece, the piece's length -------
     uint32_t bpos[U], wave_tot = 0;
+    if constexpr (GH_TILE_LMAJ) {  // lane l's segments are consecutive: one scan of their sum
+      uint32_t sl = 0;
 #pragma unroll
-    for (int u = 0; u < U; ++u) bpos[u] = wave_incl_scan(cnt[u]);
+      for (int u = 0; u < U; ++u) sl += cnt[u];
+      const uint32_t incl = wave_incl_scan(sl);
+      uint32_t run = incl - sl;
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t ct = (uint32_t)__builtin_amdgcn_readlane((int)bpos[u], 63);
-      bpos[u] += wave_tot - cnt[u];
-      wave_tot += ct;
+      for (int u = 0; u < U; ++u) {
+        bpos[u] = run;
+        run += cnt[u];
+      }
+      wave_tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) bpos[u] = wave_incl_scan(cnt[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t ct = (uint32_t)__builtin_amdgcn_readlane((int)bpos[u], 63);
+        bpos[u] += wave_tot - cnt[u];
+        wave_tot += ct;
+      }
     }
     // ---- arrival at tile k: the last wave to arrive publishes its aggregate ------------
     uint32_t tile_total = 0;
@@ -742,7 +810,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
                   lds_st_u32(ptile_lds + 4u * slot2, t2);
                 }
                 found = true;
-              } else {
+              } else if (GH_TILE_POLLDIV <= 1 || ((spins + (uint32_t)wid) % GH_TILE_POLLDIV) == 0u) {
                 pv = __hip_atomic_load(pf2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
               }
             }
@@ -835,4 +903,10 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     cur = nxt < p.ntiles ? nxt : NONE;
     nxt += G;
   }
+#if GH_TILE_STAMPS
+  if (tid == 0) {
+    wring[2] = __builtin_amdgcn_s_memtime();
+    wring[3] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
 }

@@ -102,7 +102,7 @@ class gh_raw_stream(ctypes.Structure):
 
 class gh_sync_report(ctypes.Structure):
     _fields_ = [("g", ctypes.c_uint64), ("mismatches", ctypes.c_uint64), ("passes", ctypes.c_uint32),
-                ("kernel_ms", ctypes.c_float)]
+                ("kernel_ms", ctypes.c_float), ("host_ms", ctypes.c_float), ("halo", ctypes.c_uint32)]
 
 
 MODE_NAMES = {1: "split", 2: "tile", 3: "fused", 4: "mtile"}

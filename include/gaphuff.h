@@ -241,6 +241,10 @@ typedef struct gh_sync_report {
   uint32_t passes;      /* verify/repair passes (1 when the first walk was right)  */
   float kernel_ms;      /* walk kernel to the last verify pass (HIP events; includes
                            the host turnaround between passes)                     */
+  float host_ms;        /* the halo estimate before the walk (stream sample copied
+                           back + host walks; 0 when GH_SYNC_HALO is set), wall time,
+                           not inside kernel_ms: the whole call is host_ms + kernel_ms */
+  uint32_t halo;        /* warm-up segments per lane the walk used                 */
 } gh_sync_report;
 /* Gap words (ceil(ceil(w/4)/8) u32, the gap-array file's layout) of the raw stream
  * d_words[0..w) (device memory, 16-byte aligned) into d_gap_words on `hip_stream`

@@ -36,6 +36,7 @@ for wl in sys.argv[1:] or ["cfg2", "cfg3", "cfg4"]:
             gh.sync_gaps(syms, dw.addr, s.w, dg.addr)
         reps = [gh.sync_gaps(syms, dw.addr, s.w, dg.addr) for _ in range(10)]
         sync_ms = float(np.median([x.kernel_ms for x in reps]))
+        host_ms = float(np.median([x.host_ms for x in reps]))  # the halo estimate (not in kernel_ms)
         got = dg.download(np.empty(gw, np.uint32))
     with gh.Decoder(0) as d:
         rep0 = d.load_raw(syms, n, payload)
@@ -53,6 +54,7 @@ for wl in sys.argv[1:] or ["cfg2", "cfg3", "cfg4"]:
     print(json.dumps({
         "workload": wl, "n": n, "redundancy": r, "w": s.w, "g": s.g,
         "sync_ms": round(sync_ms, 4), "sync_roofline_frac": round(alg_sync / sync_ms / 1e6 / PEAK, 3),
+        "sync_host_ms": round(host_ms, 4), "sync_call_ms": round(sync_ms + host_ms, 4), "halo": int(reps[-1].halo),
         "sync_alg_bytes": alg_sync, "mismatches": int(reps[-1].mismatches), "passes": int(reps[-1].passes),
         "decode_ms": round(rep.kernel_ms, 4), "decode_mode": gh.MODE_NAMES.get(rep.mode),
         "decode_path": gh.PATH_NAMES.get(rep.path),

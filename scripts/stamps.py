@@ -15,8 +15,9 @@ env = dict(os.environ, GAPHUFF_LIB=lib, GH_STAMPS_OUT=out)
 r = subprocess.run([sys.executable, os.path.join(here, "quick_one.py"), wl, "3"], env=env, capture_output=True,
                    text=True, timeout=300)
 print(r.stdout.strip(), r.stderr.strip()[-500:])
-a = np.fromfile(out, dtype=np.uint32)
+raw = np.fromfile(out, dtype=np.uint8)
 os.unlink(out)
+a = raw.view(np.uint32)
 grid = int(dict(x.split("=", 1) for x in r.stdout.split() if "=" in x)["grid"])
 a = a[:grid * 2 * 128 * 8].reshape(grid, 2, 128, 8).astype(np.float64)  # (then the chain times)
 names = ["load wait", "decode", "scans+arrive", "prefix", "copy-out", "stage", "-", "-"]
@@ -61,3 +62,44 @@ for label, idx in [("slowest 8", np.nonzero(sel)[0][np.argsort(busy[sel])[-8:]])
                    ("fastest 8", np.nonzero(sel)[0][np.argsort(busy[sel])[:8]])]:
     ph = (w0[idx].sum(axis=1) / iters[idx][:, None]).mean(axis=0)
     print(f"{label}: " + "  ".join(f"{n} {ph[i]:6.0f}" for i, n in enumerate(names[:6])))
+
+# ---- hand-off chain (100 MHz s_memrealtime): aggregate left -> round published (leader
+# latency) -> prefix obtained by the copying wave 0 (consumer latency); per-workgroup clock
+ntiles = int(dict(x.split("=", 1) for x in r.stdout.split() if "=" in x).get("tiles", 0) or 0)
+t = raw[32 * grid * 2 * 128:].view(np.uint64)
+if ntiles == 0:  # (quick_one does not print the tile count: from the table sizes)
+    ntiles = (t.size - 64 - 4 * 1024 - 4 * grid) // 3
+agg = t[:ntiles].astype(np.float64)
+got = (t[ntiles:2 * ntiles] & ((1 << 63) - 1)).astype(np.float64)
+D = grid - 1
+nr = (ntiles + D - 1) // D
+pub = t[2 * ntiles:2 * ntiles + nr].astype(np.float64)
+lat_lead, lat_cons, spread = [], [], []
+for rr in range(nr):
+    lo, hi = rr * D, min(ntiles, (rr + 1) * D)
+    ag = agg[lo:hi]
+    if pub[rr] == 0 or (ag == 0).any():
+        continue
+    lat_lead.append((pub[rr] - ag.max()) * 0.01)
+    spread.append((ag.max() - np.median(ag)) * 0.01)
+    g2 = got[lo:hi]
+    g2 = g2[g2 > 0]
+    lat_cons.extend(((g2 - pub[rr]) * 0.01).tolist())
+q = [10, 50, 90, 99]
+if lat_lead:
+    print("round: last aggregate - median aggregate us", np.percentile(spread, q).round(2))
+    print("round: published - last aggregate us (leader)", np.percentile(lat_lead, q).round(2))
+    lc = np.array(lat_cons)
+    print("prefix obtained - published us (consumers; < 0: seen by its own early load)",
+          np.percentile(lc, q).round(2))
+wr = t[3 * ntiles + 64 + 4 * 1024:3 * ntiles + 64 + 4 * 1024 + 4 * grid].reshape(grid, 4).astype(np.float64)
+okw = (wr[:, 3] > wr[:, 1]) & (np.arange(grid) > 0)
+clk = (wr[okw, 2] - wr[okw, 0]) / (wr[okw, 3] - wr[okw, 1]) / 10.0
+print("per-WG clock GHz pct", np.percentile(clk, [0, 10, 50, 90, 100]).round(3))
+blk2 = np.arange(grid)[okw]
+for x in range(8):
+    m = blk2 % 8 == x
+    print(f"  XCD {x}: clock {clk[m].mean():.3f} GHz, span us {((wr[okw][m, 3] - wr[okw][m, 1]) * 0.01).mean():.1f}")
+busy_ok = busy[okw] if busy.size == grid else None
+if busy_ok is not None:
+    print("corr(busy, clock)", np.corrcoef(busy_ok, clk)[0, 1].round(3))

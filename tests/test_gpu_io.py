@@ -169,8 +169,9 @@ def test_gpu_eight_shards_one_device_concurrent(gpu, tmp_path):
     """Eight shards on ONE device through the multi-shard entry points, each shard in its
     own host thread with pinned double-buffered copies: gh_decode with devices [0] * 8
     and bin/decoder --gpus 1 --shards 8 are bit-exact, and loading the eight shards from
-    eight threads takes less time than loading them one after another (their file
-    reads, staging copies and DMA overlap)."""
+    eight threads is not slower than loading them one after another, within 20 % (their
+    file reads, staging copies and DMA overlap; one device's copy engines and the shared
+    staging lease bound the gain, so a strict win is not asserted)."""
     import json
     d, path = _write(tmp_path, gpu, 8, 0.1, 160_000_000)
     img = np.fromfile(path, dtype=np.uint8)
@@ -190,6 +191,7 @@ def test_gpu_eight_shards_one_device_concurrent(gpu, tmp_path):
             assert np.array_equal(np.concatenate(parts)[: d.size], d)
     con, ser = min(times[True]), min(times[False])
     print(f"eight shards: concurrent {con:.1f} ms, one after another {ser:.1f} ms")
+    assert con < 1.2 * ser, (con, ser)
     (tmp_path / "orig.bin").write_bytes(d.tobytes())
     out = str(tmp_path / "dec.bin")
     r = subprocess.run([os.path.join(BIN, "decoder"), path, out, "--gpus", "1", "--shards", "8", "--json",

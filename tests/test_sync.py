@@ -252,9 +252,27 @@ def test_gpu_sync_halo_follows_the_stream(gpu, orc, capfd, monkeypatch):
         gaps, rep = _sync_on_gpu(gpu, pw, s.symbols)
         err = capfd.readouterr().err
         halos[r] = int(err.split("halo")[-1].split()[0])
+        assert rep.halo == halos[r]  # the report carries the halo the walk used
+        assert rep.host_ms > 0  # and the time of its estimate (not inside kernel_ms)
         gw = np.ctypeslib.as_array(ctypes.cast(s.c.gap_words, ctypes.POINTER(ctypes.c_uint32)), (gaps.size,))
         assert np.array_equal(gaps, gw)
     assert halos[0.9] <= 4 < 10 <= halos[0.5], halos
+
+
+@pytest.mark.gpu
+def test_gpu_sync_halo_saturates_when_walks_never_merge(gpu, orc, monkeypatch):
+    """A code whose walks from a wrong offset never merge (every codeword 8 bits: 7 of 8
+    sampled offsets stay out of phase for good) gives a p99.9 resync distance of 'never'.
+    The short-stream halo then saturates at its maximum (48 segments) instead of wrapping
+    to the minimum, and the verify passes still make every gap exact."""
+    monkeypatch.delenv("GH_SYNC_HALO", raising=False)
+    syms = [(i, 8) for i in range(256)]
+    d = orc.generate(3, 0.5, 300_001)
+    units = orc.raw_encode(d, syms)
+    gaps, rep = _sync_on_gpu(gpu, units, syms)
+    assert rep.halo == 48, rep.halo
+    assert rep.host_ms > 0
+    assert np.array_equal(gaps, orc.raw_gaps(d, syms))
 
 
 @pytest.mark.gpu
