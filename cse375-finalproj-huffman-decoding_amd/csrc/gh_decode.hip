@@ -885,6 +885,7 @@ extern "C" int gh_ctx_decode(gh_ctx* c, void* hip_stream, int timed) {
     t.status = c->d_misc + 1;
     t.total = (unsigned long long*)(c->d_misc + 2);
     t.stats = (unsigned long long*)(c->d_misc + 4);
+    t.tickets = (unsigned int*)(c->d_gran + 2ull * c->ntiles);  // the two spare granule words
     t.out_cap = c->out_cap;
     t.nseg = c->nseg;
     t.gap_nib0 = c->gap_nib0;

@@ -65,14 +65,33 @@ constexpr int TILE_SLOTS = 16;  // per-tile wave totals / offsets / arrival coun
 #define GH_TILE_CLDS 0  // the decode's LUT reads as plain LDS loads (the compiler's own lgkmcnt waits)
 #endif
 #ifndef GH_TILE_LMAJ
-#define GH_TILE_LMAJ 0  // lane-major segments: lane l of a wave decodes its segments U*l .. U*l + U - 1
+#define GH_TILE_LMAJ 1  // lane-major segments: lane l of a wave decodes its segments U*l .. U*l + U - 1
 #endif
 #ifndef GH_TILE_POLLDIV
 #define GH_TILE_POLLDIV 1  // a waiting wave re-polls the prefix granule every N-th spin (staggered by wave)
 #endif
+#ifndef GH_TILE_DYN
+#define GH_TILE_DYN 0  // tiles by ticket (one counter per launch parity) and a frontier leader
+#endif
+constexpr int TILE_TAHEAD = 5;  // (GH_TILE_DYN) a tile index is posted this many iterations ahead
+#ifndef GH_TILE_LATEP
+#define GH_TILE_LATEP 0  // a third prefix load right before the prefetch (see the loop)
+#endif
+#ifndef GH_TILE_EPERM
+#define GH_TILE_EPERM 0  // symbols placed into the output words as they are decoded (register peak)
+#endif
+#ifndef GH_TILE_HOLD
+#define GH_TILE_HOLD 0  // a decoded tile is held in registers one iteration and staged the next:
+                        // copy-out three iterations after the decode with two staging buffers
+#endif
+#ifndef GH_TILE_ALRD
+#define GH_TILE_ALRD 1  // copy-out: aligned LDS reads realigned in registers (see copy_out_piece)
+#endif
 #ifndef GH_TILE_ABLATE
 #define GH_TILE_ABLATE 0  // diagnostic builds only (make variant), bits: 1 no decode, 2 no staging
-                          // stores, 4 no prefix wait (a fake offset), 8 no copy-out (wrong output)
+                          // stores, 4 no prefix wait (a fake offset), 8 no copy-out, 16 even LUT
+                          // entries only (no LUT bank conflicts), 32 pieces copied out to 16-byte
+                          // aligned offsets (wrong output)
 #endif
 typedef unsigned int tile_v4u __attribute__((ext_vector_type(4)));
 // 16-byte global store of the copy-out: streaming (the output is never re-read, so it
@@ -99,6 +118,7 @@ struct TileParams {
   unsigned int stage_bytes;      // one wave's staging region (16 + its piece + margin, a multiple of 16)
   unsigned int kbits_c;          // (gh_mtile.hip) the count table's width
   unsigned int fb_hi;            // (gh_mtile.hip, codes longer than the tables) the longest codeword
+  unsigned int* tickets;         // (GH_TILE_DYN) tile counters by launch parity, 8 bytes apart
   uint4* stamps;                 // GH_TILE_STAMPS builds: [grid][2 waves][128 iterations][2] phase deltas
   unsigned long long* tstamps;   // GH_TILE_STAMPS builds: 100 MHz times: [ntiles] aggregate left, [ntiles]
                                  // prefix obtained by wave 0 (bit 63: polled), [rounds] round published
@@ -109,7 +129,7 @@ struct TileParams {
 // stage_bytes: one wave's region.
 inline size_t tile_lds_bytes(size_t lut_bytes, size_t stage_bytes) {
   return lut_bytes + TILE_LAG * (TILE_TB / 64) * stage_bytes + TILE_SLOTS * (2 * (TILE_TB / 64) + 1) * 4 +
-         TILE_SLOTS * 12 + 4 * (TILE_TB / 64) + 32;
+         TILE_SLOTS * 12 + 4 * (TILE_TB / 64) + 4 * TILE_SLOTS + 32;
 }
 
 // v_perm selector placing byte 1 of S0 (the symbol) at byte j, keeping S1's others.
@@ -239,6 +259,9 @@ __device__ __forceinline__ int decode_tile_rolling(uint32_t (&e)[U][5], const in
               : "+v"(q[u]), "+v"(cnt[u]) : "v"(ent[u]), "i"(pos + 1) : "vcc");
 #endif
           ow[u][pos >> 2] = __builtin_amdgcn_perm(ent[u], ow[u][pos >> 2], perm_sel(pos & 3));
+          // (GH_TILE_EPERM) place the symbol now: the compiler otherwise keeps every entry
+          // live until the staging, ~60 VGPRs at the decode's peak
+          if (GH_TILE_EPERM) asm volatile("" : "+v"(ow[u][pos >> 2]));
           if (!gend) {
             const uint32_t x = __builtin_amdgcn_alignbit(e[u][0], e[u][1], q[u]);
             ent[u] = lut_rd((x & amask) | laneoff);
@@ -381,7 +404,8 @@ __device__ __forceinline__ void copy_out_piece(uint8_t* out, uint32_t stg, unsig
   n = (uint32_t)__builtin_amdgcn_readfirstlane((int)n);
   const uint32_t lb = (uint32_t)(goff & 15);
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out + (goff - lb), 0, 0x7FFFFFF0, 0x00020000);
-  const uint32_t src = stg + 16u - lb;    // staging address of output chunk 0
+  // (GH_TILE_ABLATE & 128, diagnostic: 16-byte aligned LDS reads, wrong bytes)
+  const uint32_t src = stg + 16u - ((GH_TILE_ABLATE & 128) ? 0u : lb);    // staging address of output chunk 0
   const uint32_t cf = lb ? 1u : 0u;       // interior chunks [cf, ce)
   const uint32_t ce = n ? (lb + n) >> 4 : 0u;
   uint32_t off[NS];
@@ -389,8 +413,6 @@ __device__ __forceinline__ void copy_out_piece(uint8_t* out, uint32_t stg, unsig
   for (int i = 0; i < NS; ++i) {
     const uint32_t c = c0 + cf + (uint32_t)lane + 64u * (uint32_t)i;
     off[i] = c < ce ? 16u * c : OOB_OFF;
-    if (PIN) asm volatile("ds_read_b128 %0, %1" : "+v"(v[i]) : "v"(src + 16u * (c < ce ? c : cf)) : "memory");
-    else asm volatile("ds_read_b128 %0, %1" : "=v"(v[i]) : "v"(src + 16u * (c < ce ? c : cf)) : "memory");
   }
   // edge bytes: the head chunk's [lb, min(16, lb + n)) when lb != 0, then the tail
   // chunk's [0, (lb + n) & 15) when it is another chunk; one byte per lane
@@ -399,9 +421,70 @@ __device__ __forceinline__ void copy_out_piece(uint8_t* out, uint32_t stg, unsig
   const uint32_t nt = (n && tl && (ce > 0 || !lb)) ? tl : 0u;
   const uint32_t t = (uint32_t)lane;
   uint32_t k = OOB_OFF;
-  if (c0 == 0u) {
+  if (c0 == 0u && !(GH_TILE_ABLATE & 64)) {  // (diagnostic 64: no edge bytes)
     if (t < nh) k = lb + t;
     else if (t < nh + nt) k = 16u * ce + (t - nh);
+  }
+  if constexpr (GH_TILE_ALRD) {
+    // Output chunk c is staging bytes [src + 16c, +16): the last 16 - lb bytes of the
+    // aligned chunk at stg + 16c and the first lb of the next.  Both aligned chunks are read
+    // (an unaligned ds_read_b128 costs the copy-out several times its aligned pair: cfg4
+    // window 0.53 vs 0.49 ms with the reads aligned, round 6) and shifted into place in
+    // registers: output dword d = window bytes [s + 4d, +4) of P:Q, s = 16 - lb (lb = 0:
+    // Q), a wave-uniform case on s >> 2 and v_alignbyte by s & 3.  Chunks go CG at a time
+    // (registers), each group stored as soon as it is shifted; the store count is fixed.
+    constexpr int CG = NS % 2 == 0 ? 2 : 1;
+    const uint32_t sh = (16u - lb) & 15u, r = sh & 3u, m = lb ? sh >> 2 : 4u;
+#pragma unroll
+    for (int g0 = 0; g0 < NS; g0 += CG) {
+      tile_v4u pq[CG][2];
+#pragma unroll
+      for (int j = 0; j < CG; ++j) {
+        const int i = g0 + j;
+        const uint32_t c = c0 + cf + (uint32_t)lane + 64u * (uint32_t)i;
+        const uint32_t a = stg + 16u * (c < ce ? c : cf);
+        asm volatile("ds_read_b128 %0, %1" : "=v"(pq[j][0]) : "v"(a) : "memory");
+        asm volatile("ds_read_b128 %0, %1 offset:16" : "=v"(pq[j][1]) : "v"(a) : "memory");
+      }
+      if (g0 + CG >= NS) {  // the edge byte with the last group
+        if (PIN) asm volatile("ds_read_u8 %0, %1" : "+v"(b) : "v"(src + (k == OOB_OFF ? 0u : k)) : "memory");
+        else asm volatile("ds_read_u8 %0, %1" : "=v"(b) : "v"(src + (k == OOB_OFF ? 0u : k)) : "memory");
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int j = 0; j < CG; ++j) asm volatile("" : "+v"(pq[j][0]), "+v"(pq[j][1]));  // (after the wait)
+      auto shift = [&](auto mc) {
+        constexpr int M = decltype(mc)::value;
+#pragma unroll
+        for (int j = 0; j < CG; ++j) {
+          if constexpr (M == 4) {
+            v[g0 + j] = pq[j][1];
+          } else {
+            auto W = [&](int q) -> uint32_t { return q < 4 ? pq[j][0][q] : pq[j][1][q - 4]; };
+#pragma unroll
+            for (int d = 0; d < 4; ++d) v[g0 + j][d] = __builtin_amdgcn_alignbyte(W(M + d + 1), W(M + d), r);
+          }
+        }
+      };
+      switch (m) {
+        case 0: shift(std::integral_constant<int, 0>{}); break;
+        case 1: shift(std::integral_constant<int, 1>{}); break;
+        case 2: shift(std::integral_constant<int, 2>{}); break;
+        case 3: shift(std::integral_constant<int, 3>{}); break;
+        default: shift(std::integral_constant<int, 4>{}); break;
+      }
+#pragma unroll
+      for (int j = 0; j < CG; ++j) __builtin_amdgcn_raw_buffer_store_b128(v[g0 + j], rs, (int)off[g0 + j], 0, 2);  // nt
+    }
+    if (PIN) asm volatile("" : "+v"(b));
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)b, rs, (int)k, 0, 2);
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < NS; ++i) {
+    const uint32_t c = c0 + cf + (uint32_t)lane + 64u * (uint32_t)i;
+    if (PIN) asm volatile("ds_read_b128 %0, %1" : "+v"(v[i]) : "v"(src + 16u * (c < ce ? c : cf)) : "memory");
+    else asm volatile("ds_read_b128 %0, %1" : "=v"(v[i]) : "v"(src + 16u * (c < ce ? c : cf)) : "memory");
   }
   if (PIN) asm volatile("ds_read_u8 %0, %1" : "+v"(b) : "v"(src + (k == OOB_OFF ? 0u : k)) : "memory");
   else asm volatile("ds_read_u8 %0, %1" : "=v"(b) : "v"(src + (k == OOB_OFF ? 0u : k)) : "memory");
@@ -512,6 +595,77 @@ __device__ __forceinline__ void tile_round_leader(const TileParams& p, uint32_t 
   }
 }
 
+// (GH_TILE_DYN) The frontier leader: tiles are handed out by ticket, so a round of D
+// consecutive tiles may hold a tile whose workgroup waits on another tile of that round;
+// instead each tile's prefix is published as soon as every tile before it has published
+// its aggregate (a workgroup waits only on tiles older than every tile it holds, so no
+// wait cycle exists).  Per pass, thread i looks at tile F + i: the leading run of
+// aggregates already in is scanned and published, F moves past it.  Bounded like
+// poll_granule (4 s of the 100 MHz clock without progress).
+template <int TB>
+__device__ __forceinline__ void tile_frontier_leader(const TileParams& p, uint32_t* s_w, int tid, int lane, int wid) {
+  constexpr int NW = TB / 64;
+  uint32_t F = 0;
+  unsigned long long R = 0, t0 = 0;
+  uint32_t* const s_first = s_w;       // [2][NW] first tile not in, per wave (double-buffered by pass)
+  uint32_t* const s_sum = s_w + 2 * NW;  // [2][NW] wave sums
+  for (uint32_t pass = 0; F < p.ntiles; ++pass) {
+    const uint32_t t = F + (uint32_t)tid, pb = (pass & 1u) * NW;
+    bool in = false;
+    uint32_t v = 0;
+    if (t < p.ntiles) {
+      const unsigned long long g = __hip_atomic_load(&p.granules[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      in = granule_ok(p, g, 1);
+      v = (uint32_t)(g & GRAN_VMASK);
+    }
+    const unsigned long long out = __ballot(!in);
+    if (lane == 0) s_first[pb + wid] = out ? (uint32_t)__builtin_ctzll(out) : 64u;
+    __syncthreads();
+    uint32_t m = (uint32_t)TB;
+#pragma unroll
+    for (int q = NW - 1; q >= 0; --q) {
+      const uint32_t f = s_first[pb + q];
+      m = f < 64u ? 64u * (uint32_t)q + f : m;
+    }
+    const uint32_t vv = (uint32_t)tid < m ? v : 0u;
+    const uint32_t incl = wave_incl_scan(vv);
+    if (lane == 63) s_sum[pb + wid] = incl;
+    __syncthreads();
+    unsigned long long before = 0, total = 0;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+      const uint32_t x = s_sum[pb + q];
+      before += (q < wid) ? x : 0u;
+      total += x;
+    }
+    if ((uint32_t)tid < m) {
+      __hip_atomic_store(&p.prefix[t], granule(p.epoch, 2, R + before + incl - vv), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+#if GH_TILE_STAMPS
+      p.tstamps[2 * p.ntiles + t] = __builtin_amdgcn_s_memrealtime();  // tile t's prefix published
+#endif
+    }
+    R += total;
+    F += m;
+    if (m == 0u) {
+      if (tid == 0) atomicAdd(p.stats + 1, 1ull);
+      if ((pass & 63u) == 0u) {  // no progress: bounded (every thread reads the same clock)
+        if (__hip_atomic_load(p.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & GH_ST_TIMEOUT) return;
+        const unsigned long long tw = wall_clock64();
+        if (t0 == 0) {
+          t0 = tw;
+        } else if (tw - t0 > 400000000ull) {
+          if (tid == 0) atomicOr(p.status, (unsigned)GH_ST_TIMEOUT);
+          return;
+        }
+      }
+      __builtin_amdgcn_s_sleep(2);
+    } else {
+      t0 = 0;
+    }
+  }
+}
+
 // TB threads, U segments per lane, GRP codewords per window shift, OW output words per
 // segment, codewords of at least MINL bits.  Compiled for at most 4 waves per SIMD (two
 // workgroups per CU: 128 VGPRs).
@@ -537,8 +691,10 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
   unsigned long long* s_pfx = (unsigned long long*)(s_cnt + TILE_SLOTS);   // [SLOTS] prefixes (wave 0)
   uint32_t* s_ptile = (uint32_t*)(s_pfx + TILE_SLOTS);                      // [SLOTS] their tiles
   uint32_t* s_lead = s_ptile + TILE_SLOTS;                                  // [NW] (leader)
+  uint32_t* s_ring = s_lead + NW;                                           // [SLOTS] (GH_TILE_DYN) tile of iteration k
   const uint32_t cnt_lds = (uint32_t)((uint8_t*)s_cnt - smem);
   const uint32_t ptile_lds = (uint32_t)((uint8_t*)s_ptile - smem);
+  const uint32_t ring_lds = (uint32_t)((uint8_t*)s_ring - smem);
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
 #if GH_TILE_STAMPS
@@ -553,7 +709,12 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
   // decoding workgroups: every block but 0 (the leader) and p.idle_block (if < grid)
   const uint32_t D = gridDim.x - 1 - (p.idle_block < gridDim.x ? 1u : 0u);
   if (blockIdx.x == 0) {
-    tile_round_leader<TB>(p, D, s_lead, tid, lane, wid);
+    if constexpr (GH_TILE_DYN) {
+      if (tid == 0) p.tickets[2u * ((p.epoch + 1u) & 1u)] = 0u;  // the next launch's counter
+      tile_frontier_leader<TB>(p, (uint32_t*)smem, tid, lane, wid);
+    } else {
+      tile_round_leader<TB>(p, D, s_lead, tid, lane, wid);
+    }
 #if GH_TILE_STAMPS
     if (tid == 0) {
       lring[2] = __builtin_amdgcn_s_memtime();
@@ -580,9 +741,16 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
       s_cnt[tid] = 0;
       s_ptile[tid] = 0xFFFFFFFFu;
     }
+    if (GH_TILE_DYN && tid <= TILE_TAHEAD) {  // iterations 0 .. TAHEAD: static tiles
+      const uint32_t b0 = blockIdx.x - 1 - (blockIdx.x > p.idle_block ? 1u : 0u);
+      const uint32_t tt = b0 + (uint32_t)tid * D;
+      s_ring[tid] = tt < p.ntiles ? tt : 0xFFFFFFFFu;
+    }
   }
   const uint32_t S = 30u - p.kbits - p.lgr;
-  const uint32_t amask = ((1u << p.kbits) - 1u) << (2u + p.lgr);
+  // (GH_TILE_ABLATE & 16, diagnostic: even LUT entries only, so a read's lanes never
+  // collide in a bank; wrong output)
+  const uint32_t amask = (((1u << p.kbits) - 1u) << (2u + p.lgr)) & ((GH_TILE_ABLATE & 16) ? ~(1u << (2u + p.lgr)) : ~0u);
   const uint32_t laneoff = ((uint32_t)lane & ((1u << p.lgr) - 1u)) << 2;
   check_lds_base(smem, p.status);
 
@@ -590,8 +758,17 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
   const uint32_t nseg = (uint32_t)p.nseg;                 // < 2^31 (checked by the host)
   constexpr uint32_t NONE = 0xFFFFFFFFu;
   __syncthreads();  // the LUT and the counters (the last barrier of a decoding workgroup)
-  const uint32_t last_tile_k = b < p.ntiles ? (p.ntiles - 1 - b) / G : NONE;
+  // (GH_TILE_DYN: the static bound below does not hold; every iteration then either
+  // decodes a tile or drains a staged one, so 2 * ntiles iterations bound a sound run)
+  const uint32_t last_tile_k = GH_TILE_DYN ? p.ntiles + 2u * TILE_SLOTS
+                               : b < p.ntiles ? (p.ntiles - 1 - b) / G : NONE;
   uint32_t cur = b, nxt = b + G;
+  // (GH_TILE_DYN) wave 0 lane 0 holds the ticket taken one iteration earlier; tickets
+  // count tiles from (TAHEAD + 1) * D on
+  const uint32_t dyn_base = (uint32_t)(TILE_TAHEAD + 1) * D;
+  uint32_t tk = 0;
+  bool tk_live = GH_TILE_DYN && dyn_base < p.ntiles;
+  unsigned int* const tctr = GH_TILE_DYN ? p.tickets + 2u * (p.epoch & 1u) : nullptr;
   // the lane's segments in a tile: wave-contiguous, 64 per chain (chain u lane l: segment
   // 64u + l of the wave's 64U); lane-major (GH_TILE_LMAJ): lane l's U consecutive segments
   // Ul .. Ul + U - 1, so the staging stores of one instruction land ~U segments apart
@@ -624,11 +801,27 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
       }
     }
   };
+  // (GH_TILE_DYN) the ticket operation after every prefetch: wave 0 lane 0 takes the next
+  // ticket (its tile posted one iteration later), every other wave, and wave 0 once the
+  // tiles are out, issues a dropped store instead, so each wave has the same VMEM
+  // operations after its loads on every path (a counted vmcnt that never waits for the
+  // ticket, whose counter is contended: it is read a whole iteration later)
+  const __amdgpu_buffer_rsrc_t rs_out = __builtin_amdgcn_make_buffer_rsrc(p.out, 0, 0x7FFFFFF0, 0x00020000);
+  auto ticket_op = [&]() {
+    if constexpr (GH_TILE_DYN) {
+      if (wid == 0 && tk_live) {
+        if (lane == 0) tk = atomicAdd(tctr, 1u);
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)0, rs_out, (int)(OOB_OFF + 64u), 0, 2);
+      }
+    }
+  };
   load(cur);
+  ticket_op();
   {  // as many stores after these loads as every iteration issues after its prefetch
      // (the copy-out's TILE_NS + 1, dropped here: out of range): the loop's entry then
      // matches its back edge, and the compiler waits for the loads with a counted vmcnt
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(p.out, 0, 0x7FFFFFF0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs = rs_out;
 #pragma unroll
     for (int i = 0; i < TILE_NS; ++i)
       __builtin_amdgcn_raw_buffer_store_b128(tile_v4u{0, 0, 0, 0}, rs, (int)(OOB_OFF + 16u * (uint32_t)i), 0, 2);  // (distinct: not merged)
@@ -638,6 +831,16 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
   uint32_t th[TILE_LAG];          // this wave's pieces of iterations k-1 .. k-LAG (NONE: not staged)
 #pragma unroll
   for (int i = 0; i < TILE_LAG; ++i) th[i] = NONE;
+  // (GH_TILE_HOLD) the previous iteration's tile, held in registers until it is staged
+  uint32_t owp[U][OW], cntp[U], bposp[U], wtp = 0, prevt = NONE;
+  int gdp = 1;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    cntp[u] = 0;
+    bposp[u] = 0;
+#pragma unroll
+    for (int k2 = 0; k2 < OW; ++k2) asm volatile("" : "=v"(owp[u][k2]));
+  }
   uint32_t rank = 0;              // the wave's arrival rank at its last tile, in quarters
   const uint32_t region0 = stage_lds + (uint32_t)wid * p.stage_bytes;  // buffer 0; buffer 1 at + NW * stage_bytes
   const uint32_t piece_cap = p.stage_bytes - (uint32_t)(STAGE_PAD + 4 * OW + 4);
@@ -649,7 +852,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     const bool have_cur = cur < p.ntiles;
     const uint32_t t2 = th[TILE_LAG - 1];  // the piece copied out this iteration (tile k - LAG)
     const bool have2 = t2 < p.ntiles;
-    bool pending = have_cur;
+    bool pending = have_cur || (GH_TILE_HOLD && prevt < p.ntiles);
 #pragma unroll
     for (int i = 0; i < TILE_LAG; ++i) pending |= th[i] < p.ntiles;
     if (!pending) break;
@@ -657,7 +860,8 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
       if (lane == 0) atomicOr(p.status, (unsigned)GH_ST_TIMEOUT);
       break;
     }
-    const uint32_t slot = k % TILE_SLOTS, slot2 = (k + TILE_SLOTS - TILE_LAG) % TILE_SLOTS;
+    const uint32_t slot = k % TILE_SLOTS, slot2 = (k + TILE_SLOTS - TILE_LAG - GH_TILE_HOLD) % TILE_SLOTS;
+    const uint32_t slotp = (k + TILE_SLOTS - 1) % TILE_SLOTS;  // (GH_TILE_HOLD) the held tile's
     const uint32_t buf = k % TILE_LAG;
     // issue priority by the wave's arrival rank at its last tile (0: first of the
     // workgroup's waves): the waves that arrive last gate the tile's aggregate, so they
@@ -673,7 +877,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     // compiler's wait counting over such a branch fell back to vmcnt(0), which then also
     // waited for the next tile's loads issued behind it)
     unsigned long long* const pf2 = &p.prefix[have2 ? t2 : 0u];
-    unsigned long long gp0 = 0, gp = 0;
+    unsigned long long gp0 = 0, gp = 0, gpl = 0;
     if (!(GH_TILE_ABLATE & 4)) gp0 = __hip_atomic_load(pf2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     auto mid = [&]() {
       if (!(GH_TILE_ABLATE & 4)) gp = __hip_atomic_load(pf2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -717,7 +921,27 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     // copy-out instead they had ~3 K cycles, and the next decode waited ~1.3 K cycles for
     // them.  They follow the prefix loads, whose waits therefore do not include them
     // (vmcnt is one in-order queue).
+    if constexpr (GH_TILE_DYN) {
+      // wave 0 posts the tile of iteration k + 1 + TAHEAD (the ticket it took last
+      // iteration) and takes the next ticket; every wave reads the tile of iteration k + 1,
+      // posted at least TAHEAD iterations ago by wave 0, which is never more than three
+      // iterations behind another wave of its workgroup
+      if (wid == 0) {
+        uint32_t tpost = NONE;
+        if (lane == 0 && tk_live) tpost = dyn_base + tk < p.ntiles ? dyn_base + tk : NONE;
+        tpost = (uint32_t)__builtin_amdgcn_readfirstlane((int)tpost);
+        tk_live = tk_live && tpost != NONE;
+        if (lane == 0) lds_st_u32(ring_lds + 4u * ((k + 1u + TILE_TAHEAD) % TILE_SLOTS), tpost);
+      }
+      nxt = lds_ld_u32(ring_lds + 4u * ((k + 1u) % TILE_SLOTS));
+      nxt = (uint32_t)__builtin_amdgcn_readfirstlane((int)nxt);
+    }
+    // (GH_TILE_LATEP) a third look at the prefix, after the decode and just BEFORE the
+    // prefetch: vmcnt is one in-order queue, so a poll issued behind the prefetch cannot
+    // be read before the prefetch has landed (~2-3 us under load); this one can
+    if (GH_TILE_LATEP && !(GH_TILE_ABLATE & 4)) gpl = __hip_atomic_load(pf2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     load(nxt);
+    ticket_op();
     TSTAMP(2);
     // ---- wave scans: the segments' offsets in the wave's piece, the piece's length -------
     uint32_t bpos[U], wave_tot = 0;
@@ -787,8 +1011,9 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
       unsigned long long g = rfl_u64(gp0);  // wave-uniform: each waits for its own load only
       bool polled = false, got = true;  // (polled: GH_TILE_STAMPS builds)
       (void)polled;
-      if (!granule_ok(p, g, 2)) {
-        g = rfl_u64(gp);
+      if (!granule_ok(p, g, 2)) g = rfl_u64(gp);
+      if (GH_TILE_LATEP && !granule_ok(p, g, 2)) g = rfl_u64(gpl);
+      {
         if (!granule_ok(p, g, 2)) {
           polled = true;
           if (wid == 0 && lane == 0) atomicAdd(p.stats, 1ull);
@@ -834,6 +1059,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
       // its prefix: read them only now (no compiler hoisting above the check)
       asm volatile("" ::: "memory");
       goff = (g & GRAN_VMASK) + s_off[slot2 * NW + wid];
+      if (GH_TILE_ABLATE & 32) goff &= ~15ull;  // (diagnostic: 16-byte aligned pieces, wrong output)
       n2 = s_tot[slot2 * NW + wid];
       if (wid == NW - 1 && t2 == p.ntiles - 1 && got && lane == 0) *p.total = goff + n2;
 #if GH_TILE_STAMPS
@@ -856,34 +1082,57 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     // a piece larger than the region (data whose shortest codewords cluster) waits for
     // the tile's prefix instead and stores its bytes straight from registers (it has
     // published its arrival, so the prefix cannot depend on it)
-    const bool staged = have_cur && wave_tot <= piece_cap;
-    if (have_cur && !staged) {
-      unsigned long long goffc = 0;
-      bool got = true;
-      if (lane == 0) {
-        unsigned long long g = __hip_atomic_load(&p.prefix[cur], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (!granule_ok(p, g, 2)) g = poll_granule(p, &p.prefix[cur], 2);
-        got = granule_ok(p, g, 2);  // false only after a timeout (then nothing is written)
-        asm volatile("" ::: "memory");
-        goffc = (g & GRAN_VMASK) + s_off[slot * NW + wid];
-        if (wid == NW - 1 && cur == p.ntiles - 1 && got) *p.total = goffc + wave_tot;
-      }
-      goffc = rfl_u64(goffc);
-      if (__builtin_amdgcn_readfirstlane(got ? 1 : 0)) {
+    // (GH_TILE_HOLD: the tile decoded last iteration, held in registers, is staged now and
+    // this one is held in its place)
+    const uint32_t st_t = GH_TILE_HOLD ? prevt : cur;
+    const bool have_st = st_t < p.ntiles;
+    const uint32_t st_tot = GH_TILE_HOLD ? wtp : wave_tot;
+    const uint32_t st_slot = GH_TILE_HOLD ? slotp : slot;
+    const bool staged = have_st && st_tot <= piece_cap;
+    auto stage_or_store = [&](const uint32_t (&sow)[U][OW], const uint32_t (&scnt)[U], const uint32_t (&sbpos)[U],
+                              int sgd) {
+      if (have_st && !staged) {
+        unsigned long long goffc = 0;
+        bool got = true;
+        if (lane == 0) {
+          unsigned long long g = __hip_atomic_load(&p.prefix[st_t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (!granule_ok(p, g, 2)) g = poll_granule(p, &p.prefix[st_t], 2);
+          got = granule_ok(p, g, 2);  // false only after a timeout (then nothing is written)
+          asm volatile("" ::: "memory");
+          goffc = (g & GRAN_VMASK) + s_off[st_slot * NW + wid];
+          if (wid == NW - 1 && st_t == p.ntiles - 1 && got) *p.total = goffc + st_tot;
+        }
+        goffc = rfl_u64(goffc);
+        if (__builtin_amdgcn_readfirstlane(got ? 1 : 0)) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) store_direct(p.out, p.out_cap, goffc + bpos[u], ow[u], cnt[u]);
-      }
-      // (rare path) drain its data-dependent loads and stores here, so that the
-      // compiler's wait for the next tile's loads stays a counted vmcnt on the common path
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-    } else if (have_cur && !(GH_TILE_ABLATE & 2)) {
-      const uint32_t sbase = region0 + buf * NW * p.stage_bytes + STAGE_PAD;
-      uint32_t o[U];
+          for (int u = 0; u < U; ++u) store_direct(p.out, p.out_cap, goffc + sbpos[u], sow[u], scnt[u]);
+        }
+        // (rare path) drain its data-dependent loads and stores here, so that the
+        // compiler's wait for the next tile's loads stays a counted vmcnt on the common path
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      } else if (have_st && !(GH_TILE_ABLATE & 2)) {
+        const uint32_t sbase = region0 + buf * NW * p.stage_bytes + STAGE_PAD;
+        uint32_t o[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) o[u] = sbase + bpos[u];
-      // no segment of the wave holds more than GRP * gdone codewords: rounds above its
-      // last dword are skipped
-      stage_wave<U, OW>(ow, cnt, o, min(OW, (GRP * gdone + 3) >> 2));
+        for (int u = 0; u < U; ++u) o[u] = sbase + sbpos[u];
+        // no segment of the wave holds more than GRP * gdone codewords: rounds above its
+        // last dword are skipped
+        stage_wave<U, OW>(sow, scnt, o, min(OW, (GRP * sgd + 3) >> 2));
+      }
+    };
+    if constexpr (GH_TILE_HOLD) {
+      stage_or_store(owp, cntp, bposp, gdp);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        cntp[u] = cnt[u];
+        bposp[u] = bpos[u];
+#pragma unroll
+        for (int k2 = 0; k2 < OW; ++k2) owp[u][k2] = ow[u][k2];
+      }
+      wtp = wave_tot;
+      gdp = gdone;
+    } else {
+      stage_or_store(ow, cnt, bpos, gdone);
     }
     TSTAMP(6);
 #if GH_TILE_STAMPS
@@ -899,9 +1148,10 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
 #endif
 #pragma unroll
     for (int i = TILE_LAG - 1; i > 0; --i) th[i] = th[i - 1];
-    th[0] = staged ? cur : NONE;
+    th[0] = staged ? st_t : NONE;
+    if constexpr (GH_TILE_HOLD) prevt = have_cur ? cur : NONE;
     cur = nxt < p.ntiles ? nxt : NONE;
-    nxt += G;
+    if constexpr (!GH_TILE_DYN) nxt += G;
   }
 #if GH_TILE_STAMPS
   if (tid == 0) {

@@ -17,6 +17,8 @@ r = subprocess.run([sys.executable, os.path.join(here, "quick_one.py"), wl, "3"]
 print(r.stdout.strip(), r.stderr.strip()[-500:])
 raw = np.fromfile(out, dtype=np.uint8)
 os.unlink(out)
+if os.environ.get("STAMPS_KEEP"):  # the raw dump, for offline analysis
+    raw.tofile(os.environ["STAMPS_KEEP"])
 a = raw.view(np.uint32)
 grid = int(dict(x.split("=", 1) for x in r.stdout.split() if "=" in x)["grid"])
 a = a[:grid * 2 * 128 * 8].reshape(grid, 2, 128, 8).astype(np.float64)  # (then the chain times)
