@@ -87,6 +87,12 @@ constexpr int TILE_TAHEAD = 5;  // (GH_TILE_DYN) a tile index is posted this man
 #ifndef GH_TILE_ALRD
 #define GH_TILE_ALRD 1  // copy-out: aligned LDS reads realigned in registers (see copy_out_piece)
 #endif
+#ifndef GH_TILE_W2
+#define GH_TILE_W2 0  // staging rounds in dword pairs (ds_write2_b32)
+#endif
+#ifndef GH_TILE_PF2
+#define GH_TILE_PF2 0  // the tile after next prefetched (two register sets, the loop body unrolled twice)
+#endif
 #ifndef GH_TILE_ABLATE
 #define GH_TILE_ABLATE 0  // diagnostic builds only (make variant), bits: 1 no decode, 2 no staging
                           // stores, 4 no prefix wait (a fake offset), 8 no copy-out, 16 even LUT
@@ -202,6 +208,9 @@ __device__ __forceinline__ int decode_tile_rolling(uint32_t (&e)[U][5], const in
                                                    uint32_t laneoff, Mid&& mid) {
   constexpr int S = 4 * OW;
   constexpr int NG = (S + G - 1) / G;
+  // (four codewords per window shift: the deferred symbol placement kept too many entries
+  // live and spilled; placed per group instead)
+  constexpr int PLACE = GH_TILE_EPERM ? GH_TILE_EPERM : (G >= 4 ? 2 : 0);
   uint32_t q[U], ent[U];
 #if GH_TILE_CLDS
   const __attribute__((address_space(3))) uint8_t* const lds0 = (const __attribute__((address_space(3))) uint8_t*)nullptr;
@@ -261,7 +270,7 @@ __device__ __forceinline__ int decode_tile_rolling(uint32_t (&e)[U][5], const in
           ow[u][pos >> 2] = __builtin_amdgcn_perm(ent[u], ow[u][pos >> 2], perm_sel(pos & 3));
           // (GH_TILE_EPERM) place the symbol now: the compiler otherwise keeps every entry
           // live until the staging, ~60 VGPRs at the decode's peak
-          if (GH_TILE_EPERM) asm volatile("" : "+v"(ow[u][pos >> 2]));
+          if (PLACE == 1) asm volatile("" : "+v"(ow[u][pos >> 2]));
           if (!gend) {
             const uint32_t x = __builtin_amdgcn_alignbit(e[u][0], e[u][1], q[u]);
             ent[u] = lut_rd((x & amask) | laneoff);
@@ -277,6 +286,14 @@ __device__ __forceinline__ int decode_tile_rolling(uint32_t (&e)[U][5], const in
             if (!last) ent[u] = lut_rd((e[u][0] & amask) | laneoff);
           }
         }
+      }
+    }
+    if (PLACE == 2) {  // this group's symbols placed by its end
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int w0 = (gi * G) >> 2, w1 = min(OW - 1, (gi * G + G - 1) >> 2);
+#pragma unroll
+        for (int wi = w0; wi <= w1; ++wi) asm volatile("" : "+v"(ow[u][wi]));
       }
     }
     if (gi == TILE_MIDG) mid();
@@ -351,12 +368,34 @@ __device__ __forceinline__ void stage_wave(const uint32_t (&ow)[U][OW], const ui
     base[u] = o[u] - ap;
     sh[u] = 4u - ap;  // v_alignbyte amount: dword m = bytes [4m - ap, +4) of the segment
   }
+  auto dw = [&](int u, int m) { return __builtin_amdgcn_alignbyte(m < OW ? ow[u][m] : 0u, ow[u][m - 1], sh[u]); };
+  if constexpr (GH_TILE_W2) {
+    // dwords m and m - 1 of a segment in one ds_write2_b32 (rounds still descend; a
+    // segment holds >= 8 bytes, so no store of one instruction lands on another's dword)
 #pragma unroll
-  for (int m = OW; m >= 1; --m) {
-    if (m > mmax) continue;  // wave-uniform: no segment of the wave reaches dword m
+    for (int m = OW; m >= 1; m -= 2) {
+      if (m - 1 >= 1) {
+        if (m <= mmax) {
 #pragma unroll
-    for (int u = 0; u < U; ++u)
-      lds_st32_m(base[u], __builtin_amdgcn_alignbyte(m < OW ? ow[u][m] : 0u, ow[u][m - 1], sh[u]), m);
+          for (int u = 0; u < U; ++u)
+            asm volatile("ds_write2_b32 %0, %1, %2 offset0:%3 offset1:%4" ::"v"(base[u]), "v"(dw(u, m)),
+                         "v"(dw(u, m - 1)), "i"(m), "i"(m - 1) : "memory");
+        } else if (m - 1 <= mmax) {
+#pragma unroll
+          for (int u = 0; u < U; ++u) lds_st32_m(base[u], dw(u, m - 1), m - 1);
+        }
+      } else if (m <= mmax) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) lds_st32_m(base[u], dw(u, m), m);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int m = OW; m >= 1; --m) {
+      if (m > mmax) continue;  // wave-uniform: no segment of the wave reaches dword m
+#pragma unroll
+      for (int u = 0; u < U; ++u) lds_st32_m(base[u], dw(u, m), m);
+    }
   }
   // head dwords: read back (the previous segment's tail + garbage), merge, store; the
   // reads are unconditional, the stores are not (a segment at an aligned offset, and the
@@ -405,7 +444,7 @@ __device__ __forceinline__ void copy_out_piece(uint8_t* out, uint32_t stg, unsig
   const uint32_t lb = (uint32_t)(goff & 15);
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out + (goff - lb), 0, 0x7FFFFFF0, 0x00020000);
   // (GH_TILE_ABLATE & 128, diagnostic: 16-byte aligned LDS reads, wrong bytes)
-  const uint32_t src = stg + 16u - ((GH_TILE_ABLATE & 128) ? 0u : lb);    // staging address of output chunk 0
+  const uint32_t src = (stg + 16u - ((GH_TILE_ABLATE & 128) ? 0u : lb)) & ((GH_TILE_ABLATE & 256) ? ~3u : ~0u);    // staging address of output chunk 0 (diagnostic 256: dword-aligned)
   const uint32_t cf = lb ? 1u : 0u;       // interior chunks [cf, ce)
   const uint32_t ce = n ? (lb + n) >> 4 : 0u;
   uint32_t off[NS];
@@ -435,6 +474,53 @@ __device__ __forceinline__ void copy_out_piece(uint8_t* out, uint32_t stg, unsig
     // (registers), each group stored as soon as it is shifted; the store count is fixed.
     constexpr int CG = NS % 2 == 0 ? 2 : 1;
     const uint32_t sh = (16u - lb) & 15u, r = sh & 3u, m = lb ? sh >> 2 : 4u;
+    if constexpr (GH_TILE_ALRD == 2) {
+      // (variant) one aligned read per chunk: P_i = aligned chunk c_i of every lane (and
+      // P_NS for lane 0), Q_i = the next lane's P_i (lane 63: P_{i+1} of lane 0) by DPP
+      tile_v4u P[NS + 1];
+#pragma unroll
+      for (int i = 0; i <= NS; ++i) {
+        const uint32_t c = c0 + cf + (uint32_t)lane + 64u * (uint32_t)i;
+        const uint32_t a = stg + 16u * (c < ce + 1u ? c : cf);
+        asm volatile("ds_read_b128 %0, %1" : "=v"(P[i]) : "v"(a) : "memory");
+      }
+      if (PIN) asm volatile("ds_read_u8 %0, %1" : "+v"(b) : "v"(src + (k == OOB_OFF ? 0u : k)) : "memory");
+      else asm volatile("ds_read_u8 %0, %1" : "=v"(b) : "v"(src + (k == OOB_OFF ? 0u : k)) : "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int i = 0; i <= NS; ++i) asm volatile("" : "+v"(P[i]));
+#pragma unroll
+      for (int i = 0; i < NS; ++i) {
+        tile_v4u Q;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const int nx = __builtin_amdgcn_update_dpp(0, (int)P[i + 1][d], 0x134, 0xf, 0xf, false);  // wave_rol:1
+          Q[d] = (uint32_t)__builtin_amdgcn_update_dpp(nx, (int)P[i][d], 0x130, 0xf, 0xf, false);    // wave_shl:1
+        }
+        auto W = [&](int q) -> uint32_t { return q < 4 ? P[i][q] : Q[q - 4]; };
+        switch (m) {
+          case 0:
+            for (int d = 0; d < 4; ++d) v[i][d] = __builtin_amdgcn_alignbyte(W(d + 1), W(d), r);
+            break;
+          case 1:
+            for (int d = 0; d < 4; ++d) v[i][d] = __builtin_amdgcn_alignbyte(W(d + 2), W(d + 1), r);
+            break;
+          case 2:
+            for (int d = 0; d < 4; ++d) v[i][d] = __builtin_amdgcn_alignbyte(W(d + 3), W(d + 2), r);
+            break;
+          case 3:
+            for (int d = 0; d < 4; ++d) v[i][d] = __builtin_amdgcn_alignbyte(W(d + 4), W(d + 3), r);
+            break;
+          default:
+            v[i] = Q;
+            break;
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(v[i], rs, (int)off[i], 0, 2);  // nt
+      }
+      if (PIN) asm volatile("" : "+v"(b));
+      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)b, rs, (int)k, 0, 2);
+      return;
+    }
 #pragma unroll
     for (int g0 = 0; g0 < NS; g0 += CG) {
       tile_v4u pq[CG][2];
@@ -774,9 +860,15 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
   // Ul .. Ul + U - 1, so the staging stores of one instruction land ~U segments apart
   constexpr uint32_t CSTR = GH_TILE_LMAJ ? 1u : 64u;  // segment stride between chains
   const uint32_t lseg = (uint32_t)(wid * 64 * U) + (uint32_t)lane * (GH_TILE_LMAJ ? (uint32_t)U : 1u);
-  uint4 w[U];
-  uint32_t w4[U], gw[U];
-  auto load = [&](uint32_t t) {
+  constexpr int NSET = GH_TILE_PF2 ? 2 : 1;  // register sets of prefetched words
+  static_assert(!(GH_TILE_PF2 && (GH_TILE_DYN || GH_TILE_HOLD)), "PF2: static schedule, no hold");
+  uint4 wset[NSET][U];
+  uint32_t w4set[NSET][U], gwset[NSET][U];
+  auto load = [&](auto SS, uint32_t t) {
+    constexpr int SI = decltype(SS)::value;
+    uint4 (&w)[U] = wset[SI];
+    uint32_t (&w4)[U] = w4set[SI];
+    uint32_t (&gw)[U] = gwset[SI];
     const uint32_t seg0 = min(t, p.ntiles - 1) * (uint32_t)(U * TB) + lseg;
     if constexpr (GH_TILE_LMAJ) {
       // one lane's U consecutive segments: their 16 U bytes and the next segment's first
@@ -816,16 +908,25 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
       }
     }
   };
-  load(cur);
-  ticket_op();
-  {  // as many stores after these loads as every iteration issues after its prefetch
-     // (the copy-out's TILE_NS + 1, dropped here: out of range): the loop's entry then
-     // matches its back edge, and the compiler waits for the loads with a counted vmcnt
+  auto junk_stores = [&]() {  // as many stores after these loads as every iteration issues
+     // after its prefetch (the copy-out's TILE_NS + 1, dropped here: out of range): the
+     // loop's entry then matches its back edge, and the compiler waits for the loads with
+     // a counted vmcnt
     const __amdgpu_buffer_rsrc_t rs = rs_out;
 #pragma unroll
     for (int i = 0; i < TILE_NS; ++i)
       __builtin_amdgcn_raw_buffer_store_b128(tile_v4u{0, 0, 0, 0}, rs, (int)(OOB_OFF + 16u * (uint32_t)i), 0, 2);  // (distinct: not merged)
     __builtin_amdgcn_raw_buffer_store_b8((uint8_t)0, rs, (int)OOB_OFF, 0, 2);
+  };
+  load(std::integral_constant<int, 0>{}, cur);
+  ticket_op();
+  junk_stores();
+  if constexpr (GH_TILE_PF2) {
+    // (the iteration's two prefix loads, then the next tile's words: the back edge's order)
+    (void)__hip_atomic_load(&p.prefix[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    (void)__hip_atomic_load(&p.prefix[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    load(std::integral_constant<int, NSET - 1>{}, nxt);
+    junk_stores();
   }
   if (cur >= p.ntiles) cur = NONE;
   uint32_t th[TILE_LAG];          // this wave's pieces of iterations k-1 .. k-LAG (NONE: not staged)
@@ -847,7 +948,11 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
 #if GH_TILE_STAMPS
   unsigned long long ts[9];
 #endif
-  for (uint32_t k = 0;; ++k) {
+  auto body = [&](auto SS, uint32_t k) -> bool {
+    constexpr int SI = decltype(SS)::value;  // the register set holding this tile's words
+    uint4 (&w)[U] = wset[SI];
+    uint32_t (&w4)[U] = w4set[SI];
+    uint32_t (&gw)[U] = gwset[SI];
     TSTAMP(0);
     const bool have_cur = cur < p.ntiles;
     const uint32_t t2 = th[TILE_LAG - 1];  // the piece copied out this iteration (tile k - LAG)
@@ -855,10 +960,10 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     bool pending = have_cur || (GH_TILE_HOLD && prevt < p.ntiles);
 #pragma unroll
     for (int i = 0; i < TILE_LAG; ++i) pending |= th[i] < p.ntiles;
-    if (!pending) break;
+    if (!pending) return false;
     if (last_tile_k != NONE && k > last_tile_k + TILE_LAG + 2) {  // cannot happen; never hang the GPU
       if (lane == 0) atomicOr(p.status, (unsigned)GH_ST_TIMEOUT);
-      break;
+      return false;
     }
     const uint32_t slot = k % TILE_SLOTS, slot2 = (k + TILE_SLOTS - TILE_LAG - GH_TILE_HOLD) % TILE_SLOTS;
     const uint32_t slotp = (k + TILE_SLOTS - 1) % TILE_SLOTS;  // (GH_TILE_HOLD) the held tile's
@@ -940,7 +1045,8 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     // prefetch: vmcnt is one in-order queue, so a poll issued behind the prefetch cannot
     // be read before the prefetch has landed (~2-3 us under load); this one can
     if (GH_TILE_LATEP && !(GH_TILE_ABLATE & 4)) gpl = __hip_atomic_load(pf2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    load(nxt);
+    // (GH_TILE_PF2: the words of the tile after next, into this iteration's register set)
+    load(SS, GH_TILE_PF2 ? nxt + G : nxt);
     ticket_op();
     TSTAMP(2);
     // ---- wave scans: the segments' offsets in the wave's piece, the piece's length -------
@@ -1152,6 +1258,13 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     if constexpr (GH_TILE_HOLD) prevt = have_cur ? cur : NONE;
     cur = nxt < p.ntiles ? nxt : NONE;
     if constexpr (!GH_TILE_DYN) nxt += G;
+    return true;
+  };
+  for (uint32_t k = 0;; k += NSET) {
+    if (!body(std::integral_constant<int, 0>{}, k)) break;
+    if constexpr (NSET == 2) {
+      if (!body(std::integral_constant<int, NSET - 1>{}, k + 1)) break;
+    }
   }
 #if GH_TILE_STAMPS
   if (tid == 0) {
