@@ -304,8 +304,14 @@ static int mtile_setup(gh_ctx* c, double avg_seg_bytes) {
     if (const char* e = getenv("GH_MT_KC")) Kc = (uint32_t)std::clamp(atoi(e), (int)K, (int)std::min(14, 31 / gl));
     Kc = std::max(Kc, K);
   }
+  // the count table's copies (log2; GH_MT_CLGR, default 0): Kc + copies <= 14 keeps the
+  // count e-window's S >= 16
+  uint32_t clgr = 0;
+  if (const char* e = getenv("GH_MT_CLGR")) clgr = (uint32_t)std::clamp(atoi(e), 0, 3);
+  if (!GH_MT_CLUT || one) clgr = 0;
+  clgr = std::min<uint32_t>(clgr, Kc + clgr > 14 ? 14 - Kc : clgr);
   c->mt_kc = Kc;
-  const uint64_t lut_b = (GH_MT_CLUT ? (8ull << K) + (4ull << Kc) : 8ull << K)  // write table (+ count table)
+  const uint64_t lut_b = (GH_MT_CLUT ? (8ull << K) + (4ull << (Kc + clgr)) : 8ull << K)  // write table (+ count table)
                          + (fb ? (uint64_t)FB_BYTES : 0);                         // (+ fallback tables)
   const uint64_t lds_free = 160ull * 1024 - lut_b - mtile_lds_bytes(0, 0);
   // (the copy-out: 8 x 64 chunks, or 2 x 5 x 64 for codes with a 1-bit codeword)
@@ -336,10 +342,16 @@ static int mtile_setup(gh_ctx* c, double avg_seg_bytes) {
       const uint32_t b = window_codewords(cn, i, Kc, 32, &n, nullptr, &m);
       lc[i] = b | ((n ? (1u | (m << 1)) & ((1u << b) - 1u) : 0u) << 16);
     }
+    if (clgr) {  // replicated: dword i = entry i >> clgr
+      std::vector<uint32_t> lr(1u << (Kc + clgr));
+      for (uint32_t i = 0; i < lr.size(); ++i) lr[i] = lc[i >> clgr];
+      lc.swap(lr);
+    }
     std::vector<uint64_t> both(lut_b / 8);
-    const bool cfirst = (4ull << Kc) > (8ull << K);  // the larger table first (gh_mtile.hip)
-    std::memcpy((uint8_t*)both.data() + (cfirst ? 0 : 8ull << K), lc.data(), 4ull << Kc);
-    std::memcpy((uint8_t*)both.data() + (cfirst ? 4ull << Kc : 0), lt.data(), 8ull << K);
+    const uint64_t cb = 4ull << (Kc + clgr);
+    const bool cfirst = cb > (8ull << K);  // the larger table first (gh_mtile.hip)
+    std::memcpy((uint8_t*)both.data() + (cfirst ? 0 : 8ull << K), lc.data(), cb);
+    std::memcpy((uint8_t*)both.data() + (cfirst ? cb : 0), lt.data(), 8ull << K);
     lt.swap(both);
   }
   if (fb) {  // the canonical tables after the LUTs (the kernel reads the last FB_BYTES)
@@ -352,7 +364,7 @@ static int mtile_setup(gh_ctx* c, double avg_seg_bytes) {
   GH_HIP(hipMalloc(&c->d_lut_t, lut_b));
   GH_HIP(hipMemcpy(c->d_lut_t, lt.data(), lut_b, hipMemcpyHostToDevice));
   c->tile_k = K;
-  c->lgr = 0;
+  c->lgr = clgr;  // (the two-pass kernel: the count table's copies)
   c->tile_u = MT_U;
   c->ntiles = (uint32_t)ceil_div(c->nseg, (uint64_t)MT_U * MT_TB);
   c->grid = (uint32_t)std::min<uint64_t>({(uint64_t)c->ntiles + 1, (uint64_t)pc * c->num_cu, (uint64_t)LEAD_A * MT_TB});

@@ -321,11 +321,13 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
   // tables first so that each base ORs into its table's addresses; or the write table's
   // high words
   const uint32_t Kc = GH_MT_CLUT ? p.kbits_c : p.kbits;
-  const uint32_t Sc = GH_MT_CLUT ? 30u - Kc - CSH : S;
-  const uint32_t amask_c = GH_MT_CLUT ? ((1u << Kc) - 1u) << 2 : amask;
-  const bool cfirst = GH_MT_CLUT && (4u << Kc) > (8u << p.kbits);
-  const uint32_t cbase = !GH_MT_CLUT ? 4u : cfirst ? 0u : 8u << p.kbits;
-  const uint32_t wbase = cfirst ? 4u << Kc : 0u;
+  // (the count table in 2^lgr copies, lane l reading copy l mod 2^lgr: lgr = 0 by default)
+  const uint32_t Sc = GH_MT_CLUT ? 30u - Kc - CSH - p.lgr : S;
+  const uint32_t amask_c = GH_MT_CLUT ? ((1u << Kc) - 1u) << (2u + p.lgr) : amask;
+  const uint32_t cbytes = 4u << (Kc + p.lgr);
+  const bool cfirst = GH_MT_CLUT && cbytes > (8u << p.kbits);
+  const uint32_t cbase = (!GH_MT_CLUT ? 4u : cfirst ? 0u : 8u << p.kbits) | (((uint32_t)lane & ((1u << p.lgr) - 1u)) << 2);
+  const uint32_t wbase = cfirst ? cbytes : 0u;
   // (FB) the canonical tables: the last FB_BYTES of the LUT area
   const MtFb fb{(const uint32_t*)(smem + p.lut_bytes - (FB ? FB_BYTES : 0)), p.kbits + 1u, p.fb_hi};
   check_lds_base(smem, p.status);
