@@ -6,7 +6,9 @@
 // nibble (end bit mod 16) at the index of the segment it starts in, 8 nibbles per
 // u32, LSB-first.
 //
-// Kernels (input resident in HBM, 4 KiB chunks of 256 threads x 16 bytes):
+// Kernels (input resident in HBM, 8 KiB chunks of 512 threads x 16 bytes; 4 KiB of 256
+// until round 6: the write kernel's per-chunk work (two barriers, the last word's
+// completion, edge gap words) is then spread over twice the bytes, cfg4 1.05 -> 0.93 ms):
 //   gh_enc_hist_kernel   byte histogram; LDS counters replicated 32x (lane & 31), so
 //                        one instruction's lanes collide at most 2-way even on the
 //                        skewed r=0.9 data; 256 u64 atomics per workgroup.
@@ -31,6 +33,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "gaphuff.h"
@@ -38,12 +41,17 @@
 
 namespace gh {
 
-constexpr int ETB = 256;                 // threads per workgroup
+#ifndef GH_ENC_TB
+#define GH_ENC_TB 512
+#endif
+constexpr int ETB = GH_ENC_TB;           // threads per workgroup
 constexpr int EBPT = 16;                 // input bytes per thread
 constexpr int ECHUNK = ETB * EBPT;       // input bytes per chunk
 constexpr int EREP = 32;                 // histogram replicas
 // LDS image of a chunk from its gap-word-aligned base: up to 1023 bits before it,
-// 16 bits per byte, the last word's completion (< 32 + 16 bits)
+// 16 bits per byte, the last word's completion (< 32 + 16 bits).  These are the bounds;
+// the write kernel's image is sized at launch for the code's longest codeword (dynamic
+// LDS: 9-bit codes, cfg4, take 4.7 KB per 4 KiB instead of 8.3)
 constexpr int EWORDS = (1024 + ECHUNK * GH_MAX_CODE_LEN + 64) / 32 + 2;
 constexpr int EGAPW = (1024 + ECHUNK * GH_MAX_CODE_LEN) / 1024 + 2;
 
@@ -130,6 +138,21 @@ __device__ __forceinline__ uint32_t enc_block_scan(uint32_t x, uint32_t* s_red, 
 #ifndef GH_ENC_NT
 #define GH_ENC_NT 3  // (round 4: 3) write kernel, bits: 1 input loads nontemporal, 2 payload word stores nontemporal; 4 bits-kernel loads nontemporal
 #endif
+#ifndef GH_ENC_OOB
+#define GH_ENC_OOB 1  // write kernel: padding stores out of a buffer resource's range (dropped) instead of to a junk dword
+#endif
+#ifndef GH_ENC_UOR
+#define GH_ENC_UOR 1  // write kernel: a quad's first two (1: three) image words ORed unconditionally
+#endif
+#ifndef GH_ENC_LSUM
+#define GH_ENC_LSUM 1  // write kernel: lengths summed from the entries' low halves (no per-entry mask)
+#endif
+#ifndef GH_ENC_GAP2
+#define GH_ENC_GAP2 0  // write kernel: the (at most two) gap boundaries without a loop
+#endif
+#ifndef GH_ENC_GAPH
+#define GH_ENC_GAPH 0  // write kernel: gap boundaries searched per half run (two quads) instead of per run
+#endif
 #ifndef GH_ENC_BQ
 #define GH_ENC_BQ 2  // chunks in flight per thread (4 measured slower: 246 vs 229 us on cfg4)
 #endif
@@ -200,6 +223,7 @@ __global__ __launch_bounds__(ETB) void gh_enc_bits_kernel(const uint8_t* in, uin
 // block total.  gh_enc_blkscan_kernel (one workgroup): exclusive scan of the block
 // totals.  The write kernel adds the two.
 constexpr int SCAN_TB = 1024, SCAN_PT = 8, SCAN_BLK = SCAN_TB * SCAN_PT;
+static_assert((unsigned long long)SCAN_BLK * ECHUNK * 16 < (1ull << 32), "scan block bits fit u32");
 __global__ __launch_bounds__(SCAN_TB) void gh_enc_scan_kernel(const uint32_t* chunk_bits, uint32_t nchunks,
                                                               uint32_t* chunk_loc, unsigned long long* blk_tot) {
   __shared__ uint32_t s_w[SCAN_TB / 64];
@@ -214,7 +238,7 @@ __global__ __launch_bounds__(SCAN_TB) void gh_enc_scan_kernel(const uint32_t* ch
     v[k] = t;  // exclusive within the thread
     t += x;
   }
-  uint32_t incl = t;  // a block holds <= 2^29 bits (8192 chunks x 65536)
+  uint32_t incl = t;  // a block holds < 2^32 bits (8192 chunks x 16 x ECHUNK, ECHUNK <= 16 KiB)
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
     const uint32_t y = __shfl_up(incl, d, 64);
@@ -266,6 +290,7 @@ struct EncParams {
   uint32_t* junk;                      // one dword per thread of the grid (padding stores)
   uint64_t n;
   uint32_t nchunks;
+  uint32_t ewords, egapw;  // LDS image words (payload, gaps): (1024 + ECHUNK x maxlen + 64) / 32 + 2, (1024 + ECHUNK x maxlen) / 1024 + 2
 };
 
 // Write-kernel LUT replicas (lane l reads copy l mod ELREP): 16 copies collide at most
@@ -276,7 +301,13 @@ struct EncParams {
 #define GH_ENC_LREP_LONG 32
 #endif
 template <int NSW>
-constexpr int enc_lrep() { return NSW >= 6 ? GH_ENC_LREP_LONG : 16; }
+constexpr int enc_lrep() { return NSW * ETB * 4096 / ECHUNK >= 5 * 256 ? GH_ENC_LREP_LONG : 16; }  // (>= 0.3 words per input byte)
+#ifndef GH_ENC_WPE
+#define GH_ENC_WPE 4  // the write kernel's occupancy hint, waves per SIMD (6 and 8 spill)
+#endif
+// the write kernel's occupancy hint (its VGPR budget: 512 / waves per SIMD)
+template <int NSW>
+constexpr int enc_wpe() { return GH_ENC_WPE; }
 
 // A thread's 16 codewords, combined in registers: LUT entries hold the code
 // left-aligned, e = code << (32 - len) | len (len <= 16 sits in the low 5 bits, below
@@ -284,7 +315,7 @@ constexpr int enc_lrep() { return NSW >= 6 ? GH_ENC_LREP_LONG : 16; }
 // bits of the entry it shifts by), and two pairs make a left-aligned 64-bit quad.
 // Each quad is ORed into the LDS image as up to three words.
 __device__ __forceinline__ uint32_t enc_pair(uint32_t a, uint32_t c, uint32_t& len) {
-  len = (a & 31u) + (c & 31u);
+  len = GH_ENC_LSUM ? (a + c) & 0xFFFFu : (a & 31u) + (c & 31u);
   return (a & 0xFFFF0000u) | ((c & 0xFFFF0000u) >> (a & 31u));
 }
 
@@ -297,13 +328,14 @@ __device__ __forceinline__ uint32_t enc_pair(uint32_t a, uint32_t c, uint32_t& l
 // than the prefetch the next chunk waits for its loads with vmcnt(N) instead of also
 // waiting for this chunk's stores.
 template <int NSW>
-__global__ __launch_bounds__(ETB) __attribute__((amdgpu_waves_per_eu(enc_lrep<NSW>() > 16 ? 3 : 6))) void gh_enc_write_kernel(
+__global__ __launch_bounds__(ETB) __attribute__((amdgpu_waves_per_eu(enc_wpe<NSW>()))) void gh_enc_write_kernel(
     const EncParams p) {
   constexpr int ELREP = enc_lrep<NSW>();
   __shared__ uint32_t s_lutr[257 * ELREP];  // left-aligned entries, replicated
-  __shared__ uint32_t s_w[EWORDS];
-  __shared__ uint32_t s_g[EGAPW];
   __shared__ uint32_t s_red[2][ETB / 64];
+  extern __shared__ uint32_t s_dyn[];  // the image (p.ewords) and its gap words (p.egapw), sized for the code's longest codeword
+  uint32_t* const s_w = s_dyn;
+  uint32_t* const s_g = s_dyn + p.ewords;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   uint32_t c = blockIdx.x;
   const uint32_t G = gridDim.x;
@@ -333,8 +365,7 @@ __global__ __launch_bounds__(ETB) __attribute__((amdgpu_waves_per_eu(enc_lrep<NS
     const uint32_t l = v & 0xFFu;
     s_lutr[i] = l ? ((v >> 8) << (32u - l)) | l : 0u;
   }
-  for (int i = tid; i < EWORDS; i += ETB) s_w[i] = 0;
-  for (int i = tid; i < EGAPW; i += ETB) s_g[i] = 0;
+  for (uint32_t i = tid; i < p.ewords + p.egapw; i += ETB) s_dyn[i] = 0;
   __syncthreads();
   for (uint32_t it = 0; c < p.nchunks; c += G, ++it) {
     // this chunk's bytes (absent past n: 0x100, length 0)
@@ -355,8 +386,14 @@ __global__ __launch_bounds__(ETB) __attribute__((amdgpu_waves_per_eu(enc_lrep<NS
     uint32_t e[EBPT], bits = 0;
 #pragma unroll
     for (int k = 0; k < EBPT; ++k) e[k] = s_lutr[b[k] * ELREP + (tid & (ELREP - 1))];
+    if (GH_ENC_LSUM) {  // the entries' low 16 bits hold only their lengths: one sum, one mask
 #pragma unroll
-    for (int k = 0; k < EBPT; ++k) bits += e[k] & 31u;
+      for (int k = 0; k < EBPT; ++k) bits += e[k];
+      bits &= 0xFFFFu;
+    } else {
+#pragma unroll
+      for (int k = 0; k < EBPT; ++k) bits += e[k] & 31u;
+    }
     // block scan (double-buffered wave sums: the barrier also orders the previous
     // iteration's write-out and re-zeroing before this iteration's OR-s)
     const uint32_t incl = enc_wave_scan(bits);
@@ -388,30 +425,89 @@ __global__ __launch_bounds__(ETB) __attribute__((amdgpu_waves_per_eu(enc_lrep<NS
                                    ((unsigned long long)pv[2 * i + 1] << (32u - l0));
       const uint32_t hi = (uint32_t)(Q >> 32), lo = (uint32_t)Q, sft = qa & 31u;
       uint32_t* wp = &s_w[qa >> 5];
-      if (m) atomicOr(wp, hi >> sft);
-      if (sft + m > 32u) atomicOr(wp + 1, __builtin_amdgcn_alignbit(hi, lo, sft));
-      if (sft + m > 64u) atomicOr(wp + 2, __builtin_amdgcn_alignbit(lo, 0u, sft));
+      if (GH_ENC_UOR) {  // ORing zero bits is harmless: no compares, no exec-mask changes
+        atomicOr(wp, hi >> sft);
+        atomicOr(wp + 1, __builtin_amdgcn_alignbit(hi, lo, sft));
+        if (GH_ENC_UOR == 1 || sft + m > 64u) atomicOr(wp + 2, __builtin_amdgcn_alignbit(lo, 0u, sft));
+      } else {
+        if (m) atomicOr(wp, hi >> sft);
+        if (sft + m > 32u) atomicOr(wp + 1, __builtin_amdgcn_alignbit(hi, lo, sft));
+        if (sft + m > 64u) atomicOr(wp + 2, __builtin_amdgcn_alignbit(lo, 0u, sft));
+      }
       qa += m;
       qe[i] = qa;
     }
     // gap nibbles: for each 128-bit boundary strictly inside [q0, qa), the codeword
     // holding bits bd-1 and bd (quad, then pair, then codeword by compare-selects)
-    for (uint32_t bd = ((q0 >> 7) + 1u) << 7; bd < qa; bd += 128u) {
-      const bool i0 = bd >= qe[0], i1 = bd >= qe[1], i2 = bd >= qe[2];
-      const uint32_t qs4 = i2 ? qe[2] : i1 ? qe[1] : i0 ? qe[0] : q0;
-      const uint32_t la = i2 ? pl[6] : i1 ? pl[4] : i0 ? pl[2] : pl[0];
-      const uint32_t lb = i2 ? pl[7] : i1 ? pl[5] : i0 ? pl[3] : pl[1];
-      const uint32_t ea = i2 ? e[12] : i1 ? e[8] : i0 ? e[4] : e[0];
-      const uint32_t eb = i2 ? e[14] : i1 ? e[10] : i0 ? e[6] : e[2];
-      const bool second = bd >= qs4 + la;  // in the quad's second pair
-      const uint32_t ps = second ? qs4 + la : qs4;
-      const uint32_t lp = second ? lb : la;
-      const uint32_t l1 = (second ? eb : ea) & 31u;  // the pair's first codeword
-      const bool c2 = bd >= ps + l1;
-      const uint32_t cs = c2 ? ps + l1 : ps;        // codeword start
-      const uint32_t ce = c2 ? ps + lp : ps + l1;   // codeword end
-      const uint32_t gv = ce & 15u;
-      if (cs < bd && gv && cs < qend) atomicOr(&s_g[cs >> 10], gv << (4 * ((cs >> 7) & 7u)));
+    if (GH_ENC_GAPH) {
+      // (GH_ENC_GAPH) in two halves, quads 0-1 and 2-3: a half of a short-code run
+      // (<= 128 bits) holds at most one boundary, while a whole run of ~130 bits (cfg4)
+      // often holds two, which a wave then loops over for all its lanes
+      auto half = [&](uint32_t lo, uint32_t hi, uint32_t qm, auto H) {
+        constexpr int h = decltype(H)::value;  // first quad of the half
+        for (uint32_t bd = ((lo >> 7) + 1u) << 7; bd < hi; bd += 128u) {
+          const bool s1 = bd >= qm;  // in the half's second quad
+          const uint32_t qs4 = s1 ? qm : lo;
+          const uint32_t la = s1 ? pl[2 * h + 2] : pl[2 * h];
+          const uint32_t lb = s1 ? pl[2 * h + 3] : pl[2 * h + 1];
+          const uint32_t ea = s1 ? e[4 * h + 4] : e[4 * h];
+          const uint32_t eb = s1 ? e[4 * h + 6] : e[4 * h + 2];
+          const bool second = bd >= qs4 + la;
+          const uint32_t ps = second ? qs4 + la : qs4;
+          const uint32_t lp = second ? lb : la;
+          const uint32_t l1 = (second ? eb : ea) & 31u;
+          const bool c2 = bd >= ps + l1;
+          const uint32_t cs = c2 ? ps + l1 : ps;
+          const uint32_t ce = c2 ? ps + lp : ps + l1;
+          const uint32_t gv = ce & 15u;
+          if (cs < bd && gv && cs < qend) atomicOr(&s_g[cs >> 10], gv << (4 * ((cs >> 7) & 7u)));
+        }
+      };
+      half(q0, qe[1], qe[0], std::integral_constant<int, 0>{});
+      half(qe[1], qa, qe[2], std::integral_constant<int, 2>{});
+    } else if (GH_ENC_GAP2) {
+      // (GH_ENC_GAP2) at most two boundaries (a run is <= 256 bits), the second one past
+      // bit q0 + 128 and so past quads 0-1 (<= 128 bits): no loop, a two-way search
+      auto put = [&](uint32_t bd, uint32_t qs4, uint32_t la, uint32_t lb, uint32_t ea, uint32_t eb) {
+        const bool second = bd >= qs4 + la;
+        const uint32_t ps = second ? qs4 + la : qs4;
+        const uint32_t lp = second ? lb : la;
+        const uint32_t l1 = (second ? eb : ea) & 31u;
+        const bool c2 = bd >= ps + l1;
+        const uint32_t cs = c2 ? ps + l1 : ps;
+        const uint32_t ce = c2 ? ps + lp : ps + l1;
+        const uint32_t gv = ce & 15u;
+        if (cs < bd && gv && cs < qend) atomicOr(&s_g[cs >> 10], gv << (4 * ((cs >> 7) & 7u)));
+      };
+      const uint32_t bd1 = ((q0 >> 7) + 1u) << 7, bd2 = bd1 + 128u;
+      if (bd1 < qa) {
+        const bool i0 = bd1 >= qe[0], i1 = bd1 >= qe[1], i2 = bd1 >= qe[2];
+        put(bd1, i2 ? qe[2] : i1 ? qe[1] : i0 ? qe[0] : q0, i2 ? pl[6] : i1 ? pl[4] : i0 ? pl[2] : pl[0],
+            i2 ? pl[7] : i1 ? pl[5] : i0 ? pl[3] : pl[1], i2 ? e[12] : i1 ? e[8] : i0 ? e[4] : e[0],
+            i2 ? e[14] : i1 ? e[10] : i0 ? e[6] : e[2]);
+      }
+      if (bd2 < qa) {
+        const bool i2 = bd2 >= qe[2];
+        put(bd2, i2 ? qe[2] : qe[1], i2 ? pl[6] : pl[4], i2 ? pl[7] : pl[5], i2 ? e[12] : e[8], i2 ? e[14] : e[10]);
+      }
+    } else {
+      for (uint32_t bd = ((q0 >> 7) + 1u) << 7; bd < qa; bd += 128u) {
+        const bool i0 = bd >= qe[0], i1 = bd >= qe[1], i2 = bd >= qe[2];
+        const uint32_t qs4 = i2 ? qe[2] : i1 ? qe[1] : i0 ? qe[0] : q0;
+        const uint32_t la = i2 ? pl[6] : i1 ? pl[4] : i0 ? pl[2] : pl[0];
+        const uint32_t lb = i2 ? pl[7] : i1 ? pl[5] : i0 ? pl[3] : pl[1];
+        const uint32_t ea = i2 ? e[12] : i1 ? e[8] : i0 ? e[4] : e[0];
+        const uint32_t eb = i2 ? e[14] : i1 ? e[10] : i0 ? e[6] : e[2];
+        const bool second = bd >= qs4 + la;  // in the quad's second pair
+        const uint32_t ps = second ? qs4 + la : qs4;
+        const uint32_t lp = second ? lb : la;
+        const uint32_t l1 = (second ? eb : ea) & 31u;  // the pair's first codeword
+        const bool c2 = bd >= ps + l1;
+        const uint32_t cs = c2 ? ps + l1 : ps;        // codeword start
+        const uint32_t ce = c2 ? ps + lp : ps + l1;   // codeword end
+        const uint32_t gv = ce & 15u;
+        if (cs < bd && gv && cs < qend) atomicOr(&s_g[cs >> 10], gv << (4 * ((cs >> 7) & 7u)));
+      }
     }
     if (wid == ETB / 64 - 1) {
       // complete the chunk's last word (bits [qend, wend)) with the next chunk's first
@@ -433,14 +529,24 @@ __global__ __launch_bounds__(ETB) __attribute__((amdgpu_waves_per_eu(enc_lrep<NS
     const uint32_t w0 = (qs + 31u) >> 5, w1 = (qend + 31u) >> 5;
     uint32_t* wout = p.words + (B >> 5);
     uint32_t* junk = p.junk + (size_t)blockIdx.x * ETB + tid;
+    // (GH_ENC_OOB) buffer stores from the chunk's base (B is workgroup-uniform), the
+    // padding ones out of range: dropped, no memory traffic
+    const unsigned long long Bu = ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(B >> 32)) << 32) |
+                                  (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)B);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(p.words + (Bu >> 5), 0, 0x7FFFFFF0, 0x00020000);
 #pragma unroll
     for (int j = 0; j < NSW; ++j) {
       const uint32_t i = (uint32_t)tid + (uint32_t)(ETB * j);
-      const uint32_t x = s_w[i < (uint32_t)EWORDS ? i : 0u];
+      const uint32_t x = s_w[i < p.ewords ? i : 0u];
       if (i <= w1) s_w[i] = 0;
-      uint32_t* d = (i >= w0 && i < w1) ? wout + i : junk;
-      if (GH_ENC_NT & 2) __builtin_nontemporal_store(x, d);
-      else *d = x;
+      if (GH_ENC_OOB) {
+        const int off = (i >= w0 && i < w1) ? (int)(4u * i) : 0x7FFFFFF0;
+        __builtin_amdgcn_raw_buffer_store_b32(x, rw, off, 0, (GH_ENC_NT & 2) ? 2 : 0);
+      } else {
+        uint32_t* d = (i >= w0 && i < w1) ? wout + i : junk;
+        if (GH_ENC_NT & 2) __builtin_nontemporal_store(x, d);
+        else *d = x;
+      }
     }
     for (uint32_t i = tid + ETB * NSW; i <= w1; i += ETB) {
       const uint32_t x = s_w[i];
@@ -454,10 +560,15 @@ __global__ __launch_bounds__(ETB) __attribute__((amdgpu_waves_per_eu(enc_lrep<NS
     static_assert(EGAPW <= ETB, "one gap word per thread");
     {
       const uint32_t i = (uint32_t)tid;
-      const uint32_t x = s_g[i < (uint32_t)EGAPW ? i : 0u];
+      const uint32_t x = s_g[i < p.egapw ? i : 0u];
       if (i <= g1) s_g[i] = 0;
       const bool in = cbits && i <= g1, edge = i == 0 || i == g1;
-      *((in && !edge) ? gout + i : junk) = x;  // interior: a plain store (always issued)
+      if (GH_ENC_OOB) {  // interior: a plain store (always issued)
+        const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(p.gaps + (Bu >> 10), 0, 0x7FFFFFF0, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b32(x, rg, (in && !edge) ? (int)(4u * i) : 0x7FFFFFF0, 0, 0);
+      } else {
+        *((in && !edge) ? gout + i : junk) = x;
+      }
       if (in && edge && x) atomicOr(&gout[i], x);
     }
   }
@@ -622,11 +733,17 @@ extern "C" int gh_ectx_encode(gh_ectx* e, float* kernel_ms) {
                      : need <= 2 ? (const void*)gh_enc_write_kernel<2>
                      : need <= 3 ? (const void*)gh_enc_write_kernel<3>
                      : need <= 4 ? (const void*)gh_enc_write_kernel<4>
+                     : need <= 5 ? (const void*)gh_enc_write_kernel<5>
                      : need <= 6 ? (const void*)gh_enc_write_kernel<6>
                                  : (const void*)gh_enc_write_kernel<9>;
+    // the LDS image holds a chunk at the code's longest codeword
+    uint32_t maxlen = 1;
+    for (int v = 0; v < 256; ++v) maxlen = std::max<uint32_t>(maxlen, pl.len[v]);
+    const uint32_t ew = (1024u + ECHUNK * maxlen + 64u) / 32u + 2u, eg = (1024u + ECHUNK * maxlen) / 1024u + 2u;
+    const size_t dyn = 4ull * (ew + eg);
     int pb = 0, pw = 0;  // persistent grids: what is resident at once
     GH_EHIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pb, (const void*)gh_enc_bits_kernel, ETB, 0));
-    GH_EHIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pw, wk, ETB, 0));
+    GH_EHIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pw, wk, ETB, dyn));
     const uint32_t gb = (uint32_t)std::min<uint64_t>(nchunks, (uint64_t)std::max(pb, 1) * e->num_cu);
     hipLaunchKernelGGL(gh_enc_bits_kernel, dim3(gb), dim3(ETB), 0, e->stream, e->d_in, e->n, (uint32_t)nchunks,
                        e->d_lut, e->d_chunk_bits);
@@ -644,9 +761,9 @@ extern "C" int gh_ectx_encode(gh_ectx* e, float* kernel_ms) {
       GH_EHIP(hipMalloc(&e->d_junk, 4ull * gw * ETB));
       e->junk_cap = (uint64_t)gw * ETB;
     }
-    EncParams p{e->d_in, e->d_lut, loc, blk, e->d_words, e->d_gaps, e->d_junk, e->n, (uint32_t)nchunks};
+    EncParams p{e->d_in, e->d_lut, loc, blk, e->d_words, e->d_gaps, e->d_junk, e->n, (uint32_t)nchunks, ew, eg};
     void* args[] = {&p};
-    GH_EHIP(hipLaunchKernel(wk, dim3(gw), dim3(ETB), args, 0, e->stream));
+    GH_EHIP(hipLaunchKernel(wk, dim3(gw), dim3(ETB), args, dyn, e->stream));
     GH_EHIP(hipGetLastError());
   }
   GH_EHIP(hipEventRecord(e->ev1, e->stream));

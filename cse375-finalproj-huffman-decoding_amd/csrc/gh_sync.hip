@@ -69,6 +69,15 @@ constexpr int SYNC_TB = 256;    // threads per workgroup
 #endif
 constexpr uint32_t SYNC_M = GH_SYNC_M;  // segments per lane (a multiple of 8: whole gap words)
 static_assert(SYNC_M % 8 == 0, "a lane writes whole gap words");
+#ifndef GH_SYNC_RING
+#define GH_SYNC_RING 0  // walk kernel: prefetch ring of three register sets (loop unrolled by three)
+#endif
+#ifndef GH_SYNC_WPE
+#define GH_SYNC_WPE 1  // walk kernel occupancy hint (waves per SIMD; 1: the compiler's choice)
+#endif
+#ifndef GH_SYNC_RUNR
+#define GH_SYNC_RUNR 0  // in-wave repair: the block re-walk's segment loop unrolled (0: a loop)
+#endif
 // warm-up segments per lane: from the stream's resynchronisation distances (sync_halo_for;
 // GH_SYNC_HALO overrides)
 
@@ -225,7 +234,7 @@ __device__ __forceinline__ uint32_t walk_word_ls(uint32_t hi, uint32_t lo, uint3
 // vmcnt.  (Lanes crossing boundaries at different steps, each loading its next
 // segment then, made every step wait for the latest lane's loads: 1.7 ms on cfg4.)
 template <bool LONG>
-__global__ __launch_bounds__(SYNC_TB) void gh_sync_kernel(SyncParams p) {
+__global__ __launch_bounds__(SYNC_TB) __attribute__((amdgpu_waves_per_eu(GH_SYNC_WPE))) void gh_sync_kernel(SyncParams p) {
   __shared__ uint16_t lut[1 << SK];
   stage_lut(lut, p.lut);  // (the only barrier: waves past the stream may leave after it)
   const uint64_t L = (uint64_t)blockIdx.x * SYNC_TB + threadIdx.x;
@@ -234,14 +243,13 @@ __global__ __launch_bounds__(SYNC_TB) void gh_sync_kernel(SyncParams p) {
   const uint64_t se = sb < p.g ? (sb + SYNC_M < p.g ? sb + SYNC_M : p.g) : sb;  // (empty past the stream)
   const int64_t s0 = (int64_t)sb - (int64_t)p.halo;  // segment of iteration 0
   auto seg_at = [&](int64_t s) { return (uint64_t)(s < 0 ? 0 : s); };
-  SegWords w = seg_raw(seg_at(s0), p), n1 = seg_raw(seg_at(s0 + 1), p);
-  w = seg_mask(w, seg_at(s0), p);
   uint32_t pos = 0;  // segment-relative bit of the next codeword start
   uint32_t g0 = 0, g1 = 0, g2 = 0, g3 = 0, chk = 0;
   const int nit = (int)p.halo + (int)SYNC_M;
-  for (int i = 0; i < nit; ++i) {
+  // iteration i: walk segment s = s0 + i (its words loaded two iterations earlier)
+  auto body = [&](int i, const SegWords& raw) {
     const int64_t s = s0 + i;
-    const SegWords n2 = seg_raw(seg_at(s + 2), p);  // two segments ahead
+    const SegWords w = seg_mask(raw, seg_at(s), p);
     const bool act = s >= 0 && s < (int64_t)se;
     // an idle lane walks nothing: q starts past every word (and stays there)
     uint32_t q = act ? pos : 512u;
@@ -265,8 +273,30 @@ __global__ __launch_bounds__(SYNC_TB) void gh_sync_kernel(SyncParams p) {
       }
       pos = e;
     }
-    w = seg_mask(n1, seg_at(s + 1), p);
-    n1 = n2;
+  };
+  if (GH_SYNC_RING) {
+    // three register sets in rotation, the loop unrolled by three: segment s + 2 is
+    // loaded into the set that segment s - 1 used, and no set is copied, so a load is
+    // waited for two iterations after it was issued (with the copies of a two-deep
+    // prefetch, the compiler waited for it at the end of the iteration that issued it).
+    // Iterations past nit walk nothing (idle lanes).
+    SegWords X = seg_raw(seg_at(s0), p), Y = seg_raw(seg_at(s0 + 1), p), Z;
+    for (int i = 0; i < nit; i += 3) {
+      Z = seg_raw(seg_at(s0 + i + 2), p);
+      body(i, X);
+      X = seg_raw(seg_at(s0 + i + 3), p);
+      body(i + 1, Y);
+      Y = seg_raw(seg_at(s0 + i + 4), p);
+      body(i + 2, Z);
+    }
+  } else {
+    SegWords w = seg_raw(seg_at(s0), p), n1 = seg_raw(seg_at(s0 + 1), p);
+    for (int i = 0; i < nit; ++i) {
+      const SegWords n2 = seg_raw(seg_at(s0 + i + 2), p);  // two segments ahead
+      body(i, w);
+      w = n1;
+      n1 = n2;
+    }
   }
   // Verify and repair inside the wave: lane l's view of the entry at its block's start
   // (chk) against lane l-1's last nibble.  A mismatching block is re-walked from that
@@ -278,9 +308,13 @@ __global__ __launch_bounds__(SYNC_TB) void gh_sync_kernel(SyncParams p) {
     const uint32_t gw_ = k < 8 ? g0 : k < 16 ? g1 : k < 24 ? g2 : g3;
     return (gw_ >> (4 * (k & 7))) & 15u;
   };
-  auto nib_set = [&](int k, uint32_t v) {
-    uint32_t& gw_ = k < 8 ? g0 : k < 16 ? g1 : k < 24 ? g2 : g3;
-    gw_ = (gw_ & ~(15u << (4 * (k & 7)))) | (v << (4 * (k & 7)));
+  auto nib_set = [&](int k, uint32_t v) {  // (by value: a reference select put g0..g3 in scratch)
+    const uint32_t sh = 4u * (uint32_t)(k & 7), m = ~(15u << sh), x = v << sh;
+    const int q = k >> 3;
+    g0 = q == 0 ? (g0 & m) | x : g0;
+    g1 = q == 1 ? (g1 & m) | x : g1;
+    g2 = q == 2 ? (g2 & m) | x : g2;
+    g3 = q == 3 ? (g3 & m) | x : g3;
   };
   const uint32_t lane = threadIdx.x % 64;
   for (int round = 0; round < 64; ++round) {
@@ -290,7 +324,7 @@ __global__ __launch_bounds__(SYNC_TB) void gh_sync_kernel(SyncParams p) {
     if (bad) atomicAdd(p.counter + 2, 1u);  // (reported as mismatches)
     bool run = bad;
     uint32_t e = left;
-#pragma unroll
+#pragma unroll(GH_SYNC_RUNR ? GH_SYNC_M : 1)
     for (int k = 0; k < (int)SYNC_M; ++k) {
       if (!__any(run)) break;
       const uint64_t s = sb + (uint64_t)k;

@@ -4,20 +4,24 @@
 // decoupled look-back (:571-653) and second decode that writes the bytes (:655-728) — as
 // ONE decode pass per segment in one persistent kernel.
 //
-// 512-thread workgroups, U segments per lane, a tile = U * 512 consecutive segments; wave
-// w of a workgroup owns the 64 * U consecutive segments [64Uw, 64U(w+1)) of its tile, lane
-// l of chain u the segment 64Uw + 64u + l.  Workgroup 0 is the round leader; the
-// D = grid - 1 others decode: workgroup b takes tiles b, b + D, b + 2D, ... (static round
-// robin; grid <= 2048).  Iteration k of a decoding workgroup:
+// 1024-thread workgroups (16 waves), U segments per lane, a tile = U * 1024 consecutive
+// segments; wave w of a workgroup owns the 64 * U consecutive segments [64Uw, 64U(w+1))
+// of its tile, lane l the segments 64Uw + Ul .. 64Uw + Ul + U - 1 (lane-major,
+// GH_TILE_LMAJ; chain u of lane l is segment 64Uw + Ul + u).  Workgroup 0 is the round
+// leader; the D = grid - 1 others decode: workgroup b takes tiles b, b + D, b + 2D, ...
+// (static round robin; grid <= 2048).  Iteration k of a decoding workgroup, every wave
+// on its own (no workgroup barrier after the prologue):
 //
 //   decode tile k into registers (one codeword per lookup, G codewords per window shift;
 //     a codeword is kept iff it starts before the segment end: the reference's rule)
 //     - mid-decode: load the global prefix of tile k-LAG
-//   copy tile k-LAG out of staging (its prefix has had LAG-1 iterations to arrive), with a
-//     fixed store count; the next tile's loads are issued just before
-//   wave scans of the counts -> BARRIER -> publish tile k's aggregate
-//   stage tile k: every wave writes its own 64U segments (no second barrier, below); a
-//     tile larger than staging waits for its prefix and stores its bytes from registers
+//   copy tile k-LAG out of the wave's staging buffer (its prefix has had LAG-1 iterations
+//     to arrive) with a fixed store count, reading aligned 16-byte LDS chunk pairs and
+//     shifting them in registers; the next tile's loads are issued just before
+//   wave scan of the counts -> the wave's total to LDS, an LDS arrival counter; the last
+//     wave to arrive scans the 16 totals and publishes tile k's aggregate
+//   stage tile k: every wave writes its own 64U segments into its own buffer; a tile
+//     larger than staging waits for its prefix and stores its bytes from registers
 //
 // The leader takes the rounds (tiles rD .. rD + D - 1) in order: it waits for a round's
 // aggregates, scans them and publishes every tile's global exclusive prefix.  The start
@@ -753,8 +757,9 @@ __device__ __forceinline__ void tile_frontier_leader(const TileParams& p, uint32
 }
 
 // TB threads, U segments per lane, GRP codewords per window shift, OW output words per
-// segment, codewords of at least MINL bits.  Compiled for at most 4 waves per SIMD (two
-// workgroups per CU: 128 VGPRs).
+// segment, codewords of at least MINL bits.  Compiled for 4 waves per SIMD (128 VGPRs):
+// one 1024-thread workgroup per CU, which its LUT copies and staging buffers (~157 KB of
+// LDS) fill.
 //
 // The waves of a decoding workgroup run without a workgroup barrier: each stages its own
 // segments into its own LDS region and copies its own piece out.  The tile's aggregate

@@ -1,12 +1,16 @@
-# Encoder A/B: the default library against a variant (lib/libgaphuff_$1.so), cfg4 and cfg3,
-# alternating, then the encoder GPU tests on the default library.
+#!/bin/bash
+# Encoder variants side by side: bash scripts/enc_cmp.sh "cfg4 cfg3" base name ...
+# (base = the default library; name = lib/libgaphuff_name.so)
 set -o pipefail
-O=gpurun_out/${2:-r05enc}; mkdir -p $O
-L=$PWD/cse375-finalproj-huffman-decoding_amd/lib
-for i in 1 2; do
-  timeout -k 10 200 python -u scripts/bench_encode.py cfg4 cfg3 > $O/base_$i.log 2>&1 || exit 1
-  echo "base $i"; cat $O/base_$i.log
-  GAPHUFF_LIB=$L/libgaphuff_$1.so timeout -k 10 200 python -u scripts/bench_encode.py cfg4 cfg3 > $O/var_$i.log 2>&1 || exit 1
-  echo "$1 $i"; cat $O/var_$i.log
+cd "$(dirname "$0")/.." || exit 1
+wls=$1
+shift
+for v in "$@"; do
+  if [ "$v" = base ]; then unset GAPHUFF_LIB; else export GAPHUFF_LIB=$PWD/cse375-finalproj-huffman-decoding_amd/lib/libgaphuff_$v.so; fi
+  echo "== $v"
+  timeout -k 10 200 python -u scripts/bench_encode.py $wls | python3 -c '
+import json, sys
+for l in sys.stdin:
+    d = json.loads(l)
+    print("  %-5s encode_ms %.4f identical %s" % (d["workload"], d["encode_ms"], d["identical_to_host"]))' || exit 1
 done
-timeout -k 10 400 python -u -m pytest tests/test_gpu_encode.py -q -x -m gpu --timeout 120 --timeout-method thread > $O/tests.log 2>&1; tail -3 $O/tests.log
