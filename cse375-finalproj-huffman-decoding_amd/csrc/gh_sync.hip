@@ -41,9 +41,9 @@
 //                      :439-475); each pass makes at least the lowest mismatching block
 //                      true; on ordinary data the first pass finds none.
 //
-// One 13-bit LUT in LDS serves both walks: {step (the advance below, or the first
-// length when no codeword fits), length of the first codeword (0 if > 13 bits), bits of
-// the complete codewords that fit in the 13 bits (the advance)}.  Walks take the
+// One 14-bit LUT (32 KB) in LDS serves both walks: {step (the advance below, or the first
+// length when no codeword fits), length of the first codeword (0 if > 14 bits), bits of
+// the complete codewords that fit in the 14 bits (the advance)}.  Walks take the
 // multi-codeword step except where a step could skip the start that has to be
 // recorded; codes of 14-16 bits use the canonical thresholds.
 #include <hip/hip_runtime.h>
@@ -62,13 +62,22 @@
 namespace gh {
 namespace {
 
-constexpr int SK = 13;          // LUT prefix bits (12: cfg4 2.28 ms, 13: 2.08, 14: 3.10 - occupancy)
-constexpr int SYNC_TB = 256;    // threads per workgroup
+#ifndef GH_SYNC_SK
+#define GH_SYNC_SK 14  // (round 6, with the unclamped loads: cfg4 0.80 ms at 13, 0.70 at 14)
+#endif
+#ifndef GH_SYNC_TB
+#define GH_SYNC_TB 256
+#endif
+constexpr int SK = GH_SYNC_SK;       // LUT prefix bits (round 2's kernel: 12: cfg4 2.28 ms, 13: 2.08, 14: 3.10 - occupancy)
+constexpr int SYNC_TB = GH_SYNC_TB;  // threads per workgroup
 #ifndef GH_SYNC_M
 #define GH_SYNC_M 32  // (round 5: 32 with the code's own halo; 16 with 6 warm-up segments: cfg4 1.05 ms)
 #endif
 constexpr uint32_t SYNC_M = GH_SYNC_M;  // segments per lane (a multiple of 8: whole gap words)
 static_assert(SYNC_M % 8 == 0, "a lane writes whole gap words");
+#ifndef GH_SYNC_FAST
+#define GH_SYNC_FAST 1  // walk kernel: unclamped 16-byte segment loads for waves inside the stream
+#endif
 #ifndef GH_SYNC_RING
 #define GH_SYNC_RING 0  // walk kernel: prefetch ring of three register sets (loop unrolled by three)
 #endif
@@ -274,7 +283,50 @@ __global__ __launch_bounds__(SYNC_TB) __attribute__((amdgpu_waves_per_eu(GH_SYNC
       pos = e;
     }
   };
-  if (GH_SYNC_RING) {
+  // Waves whose loads all lie inside the stream (all but the last few) take them as one
+  // 16-byte load and one dword per segment from a per-lane pointer, with no clamps and
+  // no masks (the general path: five clamped dword loads, masked on use).
+  const int nitr = (nit + 2) / 3 * 3;
+  const bool fast = GH_SYNC_FAST && __all(s0 >= 0 && (uint64_t)(s0 + nitr + 1) * 4 + 5 <= p.w);
+  if (fast) {
+    const uint32_t* lw = p.words + 4 * (uint64_t)(s0 < 0 ? 0 : s0);
+    auto ld = [&](int i) {
+      const uint4 x = *reinterpret_cast<const uint4*>(lw + 4 * i);
+      return SegWords{x.x, x.y, x.z, x.w, lw[4 * i + 4]};
+    };
+    auto body_fast = [&](int i, const SegWords& w) {
+      const int64_t s = s0 + i;
+      const bool act = s < (int64_t)se;
+      uint32_t q = act ? pos : 512u;
+      q = walk_word_ls<false, LONG>(w.w0, w.w1, q, lut, p);
+      q = walk_word_ls<false, LONG>(w.w1, w.w2, q, lut, p);
+      q = walk_word_ls<false, LONG>(w.w2, w.w3, q, lut, p);
+      q = walk_word_ls<true, LONG>(w.w3, w.w4, q, lut, p);
+      if (act) {
+        uint32_t e = q;
+        if ((uint64_t)s + 1 >= p.g) e = 0;
+        if ((uint64_t)s >= sb) {
+          const uint32_t k = (uint32_t)((uint64_t)s - sb);  // (the same for every lane of the wave)
+          if (k < 8) g0 |= e << (4 * k);
+          else if (k < 16) g1 |= e << (4 * (k - 8));
+          else if (k < 24) g2 |= e << (4 * (k - 16));
+          else g3 |= e << (4 * (k - 24));
+        } else if ((uint64_t)s + 1 == sb) {
+          chk = e;
+        }
+        pos = e;
+      }
+    };
+    SegWords X = ld(0), Y = ld(1), Z;
+    for (int i = 0; i < nit; i += 3) {
+      Z = ld(i + 2);
+      body_fast(i, X);
+      X = ld(i + 3);
+      body_fast(i + 1, Y);
+      Y = ld(i + 4);
+      body_fast(i + 2, Z);
+    }
+  } else if (GH_SYNC_RING) {
     // three register sets in rotation, the loop unrolled by three: segment s + 2 is
     // loaded into the set that segment s - 1 used, and no set is copied, so a load is
     // waited for two iterations after it was issued (with the copies of a two-deep
@@ -321,7 +373,11 @@ __global__ __launch_bounds__(SYNC_TB) __attribute__((amdgpu_waves_per_eu(GH_SYNC
     const uint32_t left = (uint32_t)__shfl_up((int)nib_get(SYNC_M - 1), 1);
     const bool bad = lane > 0 && sb < p.g && chk != left;
     if (!__any(bad)) break;
-    if (bad) atomicAdd(p.counter + 2, 1u);  // (reported as mismatches)
+    {  // (reported as mismatches) one atomic per wave: per lane, the same-address atomics
+       // of a stream with many mismatching blocks serialised (cfg4 at halo 0: 18.8 ms)
+      const unsigned long long bm = __ballot(bad);
+      if (lane == 0) atomicAdd(p.counter + 2, (unsigned)__popcll(bm));
+    }
     bool run = bad;
     uint32_t e = left;
 #pragma unroll(GH_SYNC_RUNR ? GH_SYNC_M : 1)
@@ -406,15 +462,24 @@ __global__ __launch_bounds__(SYNC_TB) void gh_sync_fix_kernel(SyncParams p) {
   stage_lut(lut, p.lut);
   const uint64_t nb = ceil_div_d(p.g, SYNC_M), nwv = ceil_div_d(nb, 64);
   const uint64_t stride = (uint64_t)gridDim.x * SYNC_TB;
+  uint32_t nrep = 0, nlast = 0;  // (summed per wave: one atomic each)
   for (uint64_t k = (uint64_t)blockIdx.x * SYNC_TB + threadIdx.x + 1; k < nwv; k += stride) {
     const uint64_t L1 = min(64 * k + 64, nb);
     for (uint64_t L = 64 * k; L < L1; ++L) {
       const uint32_t a = nib_at(p.gaps, L * SYNC_M - 1);  // block L-1's entry at boundary L * M
       if (p.check[L] == a) break;
-      atomicAdd(p.counter, 1u);
+      ++nrep;
       repair_block<LONG>(L, a, lut, p);
-      if (L + 1 == L1) atomicAdd(p.counter + 1, 1u);
+      if (L + 1 == L1) ++nlast;
     }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    nrep += (uint32_t)__shfl_xor((int)nrep, o);
+    nlast += (uint32_t)__shfl_xor((int)nlast, o);
+  }
+  if (threadIdx.x % 64 == 0) {
+    if (nrep) atomicAdd(p.counter, nrep);
+    if (nlast) atomicAdd(p.counter + 1, nlast);
   }
 }
 

@@ -3,7 +3,8 @@
 # first verify pass, HIP events; input resident in HBM) and the gap-array decode of the
 # stream loaded through gh_ctx_load_raw; checks the synthesised gap words against the
 # encoder's and the decoded bytes against the input.
-# Usage: python scripts/bench_sync.py [cfg2 cfg3 cfg4]   (prints one JSON line each)
+# Usage: python scripts/bench_sync.py [--halo H] [cfg2 cfg3 cfg4]   (prints one JSON line each;
+# --halo forces the warm-up segments per lane, GH_SYNC_HALO, e.g. 0 for many repairs)
 import ctypes
 import json
 import os
@@ -22,7 +23,13 @@ def arr(ptr, n):
     return np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ctypes.c_uint32)), (max(n, 1),))[:n]
 
 
-for wl in sys.argv[1:] or ["cfg2", "cfg3", "cfg4"]:
+args = sys.argv[1:]
+forced = None
+if args[:1] == ["--halo"]:
+    forced = args[1]
+    os.environ["GH_SYNC_HALO"] = forced
+    args = args[2:]
+for wl in args or ["cfg2", "cfg3", "cfg4"]:
     n, r = WORKLOADS[wl]
     data = gh.generate(375, r, n)
     s = gh.parse(gh.encode(data, threads=16))
@@ -52,7 +59,7 @@ for wl in sys.argv[1:] or ["cfg2", "cfg3", "cfg4"]:
     alg_dec = 4 * s.w + 4 * gw + n
     total = sync_ms + rep.kernel_ms
     print(json.dumps({
-        "workload": wl, "n": n, "redundancy": r, "w": s.w, "g": s.g,
+        "workload": wl, "n": n, "redundancy": r, "w": s.w, "g": s.g, "halo_forced": forced is not None,
         "sync_ms": round(sync_ms, 4), "sync_roofline_frac": round(alg_sync / sync_ms / 1e6 / PEAK, 3),
         "sync_host_ms": round(host_ms, 4), "sync_call_ms": round(sync_ms + host_ms, 4), "halo": int(reps[-1].halo),
         "sync_alg_bytes": alg_sync, "mismatches": int(reps[-1].mismatches), "passes": int(reps[-1].passes),

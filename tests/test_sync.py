@@ -276,6 +276,28 @@ def test_gpu_sync_halo_saturates_when_walks_never_merge(gpu, orc, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("halo", ["0", "1"])
+def test_gpu_sync_forced_small_halo_many_repairs(gpu, orc, halo, monkeypatch):
+    """A 4 MB r = 0.5 stream (slow-merging code: walks from a wrong bit need ~330 bits on
+    average, p99 ~2400) with the warm-up forced down to 0-1 segments: a large share of the
+    blocks fail verification and are re-walked inside their waves (and across waves by the
+    fix pass), and the gaps still equal the encoder's, the decode the input.  The time of
+    this case at 10^8 B is recorded by scripts/bench_sync.py --halo (profiles/r06_sync.jsonl)."""
+    monkeypatch.setenv("GH_SYNC_HALO", halo)
+    import ctypes
+    d = gpu.generate(23, 0.5, 4_000_000)
+    s = gpu.parse(gpu.encode(d))
+    pw = np.ctypeslib.as_array(ctypes.cast(s.c.payload, ctypes.POINTER(ctypes.c_uint32)), (s.w,)).copy()
+    gaps, rep = _sync_on_gpu(gpu, pw, s.symbols)
+    nblk = (s.g + 31) // 32
+    assert rep.halo == int(halo)
+    assert rep.mismatches > nblk // 20, (rep.mismatches, nblk)  # many repairs, not a few
+    gw = np.ctypeslib.as_array(ctypes.cast(s.c.gap_words, ctypes.POINTER(ctypes.c_uint32)), (gaps.size,))
+    assert np.array_equal(gaps, gw)
+    assert np.array_equal(gpu.decode_raw(pw, s.symbols, d.size), d)
+
+
+@pytest.mark.gpu
 def test_gpu_decode_raw_empty(gpu):
     with gpu.Decoder(0) as dec:
         rep = dec.load_raw([(65, 1)], 0, np.zeros(0, np.uint32))
