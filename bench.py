@@ -160,7 +160,10 @@ def load_traffic(workload: str, per_gpu: int, n_gpus: int):
         with open(path) as f:
             t = json.load(f)
         e = t.get(f"{workload}_{per_gpu}_n{n_gpus}")
-        return (None, None) if e is None else (float(e["bytes_per_launch"]), e.get("source"))
+        if e is None:
+            return None, None
+        # the source names the kernel(s) the counters were read from first
+        return float(e["bytes_per_launch"]), f"{' + '.join(e.get('kernels', []))} (round {e.get('round')}): {e.get('source')}"
     except (OSError, ValueError, KeyError):
         return None, None
 

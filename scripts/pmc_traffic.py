@@ -35,6 +35,7 @@ for arg in sys.argv[2:]:
         "fetch_size_kib_per_decode": fetch,
         "write_size_kib_per_decode": write,
         "kernels": sorted(per["FETCH_SIZE"]),
+        "round": int(os.environ.get("PMC_ROUND", "0")) or None,
         "source": f"{fdir.rstrip('/')}+{os.path.basename(wdir.rstrip('/'))}: "
                   "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of "
                   + os.environ.get("PMC_CMD", f"`python3 bench.py --workload {wl.split('_')[0]} --cpu-sample 0 --no-copy`")

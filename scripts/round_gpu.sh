@@ -18,10 +18,10 @@ case ${1:-a} in
       "bench cfg3 --workload cfg3 --sub none --cpu-sample 0" "bench cfg2 --workload cfg2 --sub none --cpu-sample 0" ;;
   b)
     bash scripts/lease.sh "$O" "stats cfg4 cfg4" "stats cfg3 cfg3" "stats cfg5 cfg5" "stats cfg2 cfg2" \
-      "traffic cfg4 cfg4" "traffic cfg3 cfg3" "traffic cfg5 cfg5" "sq cfg4 cfg4" ;;
+      "traffic cfg4 cfg4" "traffic cfg3 cfg3" "traffic cfg5 cfg5" "traffic cfg2 cfg2" "sq cfg4 cfg4" "sq cfg3 cfg3" ;;
   c)
     bash scripts/lease.sh "$O" "cmd encode 300 python -u scripts/bench_encode.py" \
-      "cmd sync 300 python -u scripts/bench_sync.py" "cmd longcodes 500 python -u scripts/time_longcodes.py" \
+      "cmd sync 300 python -u scripts/bench_sync.py" "cmd longcodes 500 python -u scripts/time_longcodes.py --q 0.5,0.6,0.7" \
       "cmd shards 300 python -u scripts/bench_shards.py" ;;
   bc)
     bash scripts/round_gpu.sh b && bash scripts/round_gpu.sh c ;;
