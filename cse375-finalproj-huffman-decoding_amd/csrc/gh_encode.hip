@@ -153,6 +153,9 @@ __device__ __forceinline__ uint32_t enc_block_scan(uint32_t x, uint32_t* s_red, 
 #ifndef GH_ENC_GAPH
 #define GH_ENC_GAPH 0  // write kernel: gap boundaries searched per half run (two quads) instead of per run
 #endif
+#ifndef GH_ENC_WSUB
+#define GH_ENC_WSUB 0  // bits kernel: per-wave sums (ETB / 64 per chunk, added by the scan kernel), no barrier
+#endif
 #ifndef GH_ENC_BQ
 #define GH_ENC_BQ 2  // chunks in flight per thread (4 measured slower: 246 vs 229 us on cfg4)
 #endif
@@ -202,6 +205,15 @@ __global__ __launch_bounds__(ETB) void gh_enc_bits_kernel(const uint8_t* in, uin
     for (int j = 0; j < EBQ; ++j) b[j] = chunk_bits_of(v[j], c + (uint32_t)j * G);
 #pragma unroll
     for (int j = 0; j < EBQ; ++j) v[j] = ld(c + (uint32_t)(EBQ + j) * G);
+    if (GH_ENC_WSUB) {  // each wave's 1 KiB sum on its own: no barrier (the scan kernel adds them)
+#pragma unroll
+      for (int j = 0; j < EBQ; ++j) {
+        const uint32_t sc = enc_wave_scan(b[j]);
+        const uint32_t cc = c + (uint32_t)j * G;
+        if (lane == 63 && cc < nchunks) chunk_bits[(size_t)cc * (ETB / 64) + wid] = sc;
+      }
+      continue;
+    }
 #pragma unroll
     for (int j = 0; j < EBQ; ++j) {
       const uint32_t sc = enc_wave_scan(b[j]);  // lane 63: the wave total
@@ -231,7 +243,17 @@ __global__ __launch_bounds__(SCAN_TB) void gh_enc_scan_kernel(const uint32_t* ch
   const uint32_t i0 = blockIdx.x * (uint32_t)SCAN_BLK + (uint32_t)tid * SCAN_PT;
   uint32_t v[SCAN_PT], t = 0;
 #pragma unroll
-  for (int k = 0; k < SCAN_PT; ++k) v[k] = i0 + k < nchunks ? chunk_bits[i0 + k] : 0u;
+  for (int k = 0; k < SCAN_PT; ++k) {
+    if (GH_ENC_WSUB) {  // the chunk's per-wave sums
+      uint32_t x = 0;
+      if (i0 + k < nchunks)
+#pragma unroll
+        for (int q = 0; q < ETB / 64; ++q) x += chunk_bits[(size_t)(i0 + k) * (ETB / 64) + q];
+      v[k] = x;
+    } else {
+      v[k] = i0 + k < nchunks ? chunk_bits[i0 + k] : 0u;
+    }
+  }
 #pragma unroll
   for (int k = 0; k < SCAN_PT; ++k) {
     const uint32_t x = v[k];
@@ -703,7 +725,7 @@ extern "C" int gh_ectx_encode(gh_ectx* e, float* kernel_ms) {
     e->d_chunk_bits = nullptr;
     e->d_chunk_off = nullptr;
     e->chunk_cap = 0;
-    GH_EHIP(hipMalloc(&e->d_chunk_bits, 4 * (nchunks + 1)));
+    GH_EHIP(hipMalloc(&e->d_chunk_bits, 4 * (nchunks + 1) * (GH_ENC_WSUB ? ETB / 64 : 1)));
     GH_EHIP(hipMalloc(&e->d_chunk_off, 4 * (nchunks + 1) + 8 * (nchunks / SCAN_BLK + 2) + 64));
     e->chunk_cap = nchunks + 1;
   }
