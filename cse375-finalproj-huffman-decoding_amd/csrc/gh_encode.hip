@@ -33,7 +33,6 @@
 #include <hip/hip_runtime.h>
 
 #include <cstring>
-#include <type_traits>
 #include <vector>
 
 #include "gaphuff.h"
@@ -147,15 +146,6 @@ __device__ __forceinline__ uint32_t enc_block_scan(uint32_t x, uint32_t* s_red, 
 #ifndef GH_ENC_LSUM
 #define GH_ENC_LSUM 1  // write kernel: lengths summed from the entries' low halves (no per-entry mask)
 #endif
-#ifndef GH_ENC_GAP2
-#define GH_ENC_GAP2 0  // write kernel: the (at most two) gap boundaries without a loop
-#endif
-#ifndef GH_ENC_GAPH
-#define GH_ENC_GAPH 0  // write kernel: gap boundaries searched per half run (two quads) instead of per run
-#endif
-#ifndef GH_ENC_WSUB
-#define GH_ENC_WSUB 0  // bits kernel: per-wave sums (ETB / 64 per chunk, added by the scan kernel), no barrier
-#endif
 #ifndef GH_ENC_BQ
 #define GH_ENC_BQ 2  // chunks in flight per thread (4 measured slower: 246 vs 229 us on cfg4)
 #endif
@@ -205,15 +195,6 @@ __global__ __launch_bounds__(ETB) void gh_enc_bits_kernel(const uint8_t* in, uin
     for (int j = 0; j < EBQ; ++j) b[j] = chunk_bits_of(v[j], c + (uint32_t)j * G);
 #pragma unroll
     for (int j = 0; j < EBQ; ++j) v[j] = ld(c + (uint32_t)(EBQ + j) * G);
-    if (GH_ENC_WSUB) {  // each wave's 1 KiB sum on its own: no barrier (the scan kernel adds them)
-#pragma unroll
-      for (int j = 0; j < EBQ; ++j) {
-        const uint32_t sc = enc_wave_scan(b[j]);
-        const uint32_t cc = c + (uint32_t)j * G;
-        if (lane == 63 && cc < nchunks) chunk_bits[(size_t)cc * (ETB / 64) + wid] = sc;
-      }
-      continue;
-    }
 #pragma unroll
     for (int j = 0; j < EBQ; ++j) {
       const uint32_t sc = enc_wave_scan(b[j]);  // lane 63: the wave total
@@ -243,17 +224,7 @@ __global__ __launch_bounds__(SCAN_TB) void gh_enc_scan_kernel(const uint32_t* ch
   const uint32_t i0 = blockIdx.x * (uint32_t)SCAN_BLK + (uint32_t)tid * SCAN_PT;
   uint32_t v[SCAN_PT], t = 0;
 #pragma unroll
-  for (int k = 0; k < SCAN_PT; ++k) {
-    if (GH_ENC_WSUB) {  // the chunk's per-wave sums
-      uint32_t x = 0;
-      if (i0 + k < nchunks)
-#pragma unroll
-        for (int q = 0; q < ETB / 64; ++q) x += chunk_bits[(size_t)(i0 + k) * (ETB / 64) + q];
-      v[k] = x;
-    } else {
-      v[k] = i0 + k < nchunks ? chunk_bits[i0 + k] : 0u;
-    }
-  }
+  for (int k = 0; k < SCAN_PT; ++k) v[k] = i0 + k < nchunks ? chunk_bits[i0 + k] : 0u;
 #pragma unroll
   for (int k = 0; k < SCAN_PT; ++k) {
     const uint32_t x = v[k];
@@ -461,75 +432,22 @@ __global__ __launch_bounds__(ETB) __attribute__((amdgpu_waves_per_eu(enc_wpe<NSW
     }
     // gap nibbles: for each 128-bit boundary strictly inside [q0, qa), the codeword
     // holding bits bd-1 and bd (quad, then pair, then codeword by compare-selects)
-    if (GH_ENC_GAPH) {
-      // (GH_ENC_GAPH) in two halves, quads 0-1 and 2-3: a half of a short-code run
-      // (<= 128 bits) holds at most one boundary, while a whole run of ~130 bits (cfg4)
-      // often holds two, which a wave then loops over for all its lanes
-      auto half = [&](uint32_t lo, uint32_t hi, uint32_t qm, auto H) {
-        constexpr int h = decltype(H)::value;  // first quad of the half
-        for (uint32_t bd = ((lo >> 7) + 1u) << 7; bd < hi; bd += 128u) {
-          const bool s1 = bd >= qm;  // in the half's second quad
-          const uint32_t qs4 = s1 ? qm : lo;
-          const uint32_t la = s1 ? pl[2 * h + 2] : pl[2 * h];
-          const uint32_t lb = s1 ? pl[2 * h + 3] : pl[2 * h + 1];
-          const uint32_t ea = s1 ? e[4 * h + 4] : e[4 * h];
-          const uint32_t eb = s1 ? e[4 * h + 6] : e[4 * h + 2];
-          const bool second = bd >= qs4 + la;
-          const uint32_t ps = second ? qs4 + la : qs4;
-          const uint32_t lp = second ? lb : la;
-          const uint32_t l1 = (second ? eb : ea) & 31u;
-          const bool c2 = bd >= ps + l1;
-          const uint32_t cs = c2 ? ps + l1 : ps;
-          const uint32_t ce = c2 ? ps + lp : ps + l1;
-          const uint32_t gv = ce & 15u;
-          if (cs < bd && gv && cs < qend) atomicOr(&s_g[cs >> 10], gv << (4 * ((cs >> 7) & 7u)));
-        }
-      };
-      half(q0, qe[1], qe[0], std::integral_constant<int, 0>{});
-      half(qe[1], qa, qe[2], std::integral_constant<int, 2>{});
-    } else if (GH_ENC_GAP2) {
-      // (GH_ENC_GAP2) at most two boundaries (a run is <= 256 bits), the second one past
-      // bit q0 + 128 and so past quads 0-1 (<= 128 bits): no loop, a two-way search
-      auto put = [&](uint32_t bd, uint32_t qs4, uint32_t la, uint32_t lb, uint32_t ea, uint32_t eb) {
-        const bool second = bd >= qs4 + la;
-        const uint32_t ps = second ? qs4 + la : qs4;
-        const uint32_t lp = second ? lb : la;
-        const uint32_t l1 = (second ? eb : ea) & 31u;
-        const bool c2 = bd >= ps + l1;
-        const uint32_t cs = c2 ? ps + l1 : ps;
-        const uint32_t ce = c2 ? ps + lp : ps + l1;
-        const uint32_t gv = ce & 15u;
-        if (cs < bd && gv && cs < qend) atomicOr(&s_g[cs >> 10], gv << (4 * ((cs >> 7) & 7u)));
-      };
-      const uint32_t bd1 = ((q0 >> 7) + 1u) << 7, bd2 = bd1 + 128u;
-      if (bd1 < qa) {
-        const bool i0 = bd1 >= qe[0], i1 = bd1 >= qe[1], i2 = bd1 >= qe[2];
-        put(bd1, i2 ? qe[2] : i1 ? qe[1] : i0 ? qe[0] : q0, i2 ? pl[6] : i1 ? pl[4] : i0 ? pl[2] : pl[0],
-            i2 ? pl[7] : i1 ? pl[5] : i0 ? pl[3] : pl[1], i2 ? e[12] : i1 ? e[8] : i0 ? e[4] : e[0],
-            i2 ? e[14] : i1 ? e[10] : i0 ? e[6] : e[2]);
-      }
-      if (bd2 < qa) {
-        const bool i2 = bd2 >= qe[2];
-        put(bd2, i2 ? qe[2] : qe[1], i2 ? pl[6] : pl[4], i2 ? pl[7] : pl[5], i2 ? e[12] : e[8], i2 ? e[14] : e[10]);
-      }
-    } else {
-      for (uint32_t bd = ((q0 >> 7) + 1u) << 7; bd < qa; bd += 128u) {
-        const bool i0 = bd >= qe[0], i1 = bd >= qe[1], i2 = bd >= qe[2];
-        const uint32_t qs4 = i2 ? qe[2] : i1 ? qe[1] : i0 ? qe[0] : q0;
-        const uint32_t la = i2 ? pl[6] : i1 ? pl[4] : i0 ? pl[2] : pl[0];
-        const uint32_t lb = i2 ? pl[7] : i1 ? pl[5] : i0 ? pl[3] : pl[1];
-        const uint32_t ea = i2 ? e[12] : i1 ? e[8] : i0 ? e[4] : e[0];
-        const uint32_t eb = i2 ? e[14] : i1 ? e[10] : i0 ? e[6] : e[2];
-        const bool second = bd >= qs4 + la;  // in the quad's second pair
-        const uint32_t ps = second ? qs4 + la : qs4;
-        const uint32_t lp = second ? lb : la;
-        const uint32_t l1 = (second ? eb : ea) & 31u;  // the pair's first codeword
-        const bool c2 = bd >= ps + l1;
-        const uint32_t cs = c2 ? ps + l1 : ps;        // codeword start
-        const uint32_t ce = c2 ? ps + lp : ps + l1;   // codeword end
-        const uint32_t gv = ce & 15u;
-        if (cs < bd && gv && cs < qend) atomicOr(&s_g[cs >> 10], gv << (4 * ((cs >> 7) & 7u)));
-      }
+    for (uint32_t bd = ((q0 >> 7) + 1u) << 7; bd < qa; bd += 128u) {
+      const bool i0 = bd >= qe[0], i1 = bd >= qe[1], i2 = bd >= qe[2];
+      const uint32_t qs4 = i2 ? qe[2] : i1 ? qe[1] : i0 ? qe[0] : q0;
+      const uint32_t la = i2 ? pl[6] : i1 ? pl[4] : i0 ? pl[2] : pl[0];
+      const uint32_t lb = i2 ? pl[7] : i1 ? pl[5] : i0 ? pl[3] : pl[1];
+      const uint32_t ea = i2 ? e[12] : i1 ? e[8] : i0 ? e[4] : e[0];
+      const uint32_t eb = i2 ? e[14] : i1 ? e[10] : i0 ? e[6] : e[2];
+      const bool second = bd >= qs4 + la;  // in the quad's second pair
+      const uint32_t ps = second ? qs4 + la : qs4;
+      const uint32_t lp = second ? lb : la;
+      const uint32_t l1 = (second ? eb : ea) & 31u;  // the pair's first codeword
+      const bool c2 = bd >= ps + l1;
+      const uint32_t cs = c2 ? ps + l1 : ps;        // codeword start
+      const uint32_t ce = c2 ? ps + lp : ps + l1;   // codeword end
+      const uint32_t gv = ce & 15u;
+      if (cs < bd && gv && cs < qend) atomicOr(&s_g[cs >> 10], gv << (4 * ((cs >> 7) & 7u)));
     }
     if (wid == ETB / 64 - 1) {
       // complete the chunk's last word (bits [qend, wend)) with the next chunk's first
@@ -725,7 +643,7 @@ extern "C" int gh_ectx_encode(gh_ectx* e, float* kernel_ms) {
     e->d_chunk_bits = nullptr;
     e->d_chunk_off = nullptr;
     e->chunk_cap = 0;
-    GH_EHIP(hipMalloc(&e->d_chunk_bits, 4 * (nchunks + 1) * (GH_ENC_WSUB ? ETB / 64 : 1)));
+    GH_EHIP(hipMalloc(&e->d_chunk_bits, 4 * (nchunks + 1)));
     GH_EHIP(hipMalloc(&e->d_chunk_off, 4 * (nchunks + 1) + 8 * (nchunks / SCAN_BLK + 2) + 64));
     e->chunk_cap = nchunks + 1;
   }

@@ -61,6 +61,25 @@ def test_long_codes_and_all_gap_values(gpu, orc):
     assert len(nib) >= 12
 
 
+@pytest.mark.parametrize("r", [0.1, 0.5])
+@pytest.mark.parametrize("n", [8191, 8192, 8193, 16383, 16385, 24577])
+def test_chunk_edges(gpu, orc, r, n):
+    """Round 6: 8 KiB chunks of 512 threads: sizes around one, two and three chunks."""
+    _check(gpu, orc, gpu.generate(3000 + n, r, n))
+
+
+def test_chunks_of_longest_codewords(gpu, orc):
+    """The write kernel's LDS image is sized at launch for the code's longest codeword: a
+    run of 16 KiB of rare symbols (15-16-bit codewords) in a skewed stream fills two whole
+    chunks' images close to that bound."""
+    rng = np.random.default_rng(19)
+    data = np.minimum(rng.geometric(0.5, 4_000_000) - 1, 40).astype(np.uint8)
+    data[1_000_000:1_000_000 + 16384] = (np.arange(16384) % 200 + 50).astype(np.uint8)
+    img = _check(gpu, orc, data)
+    s = gpu.parse(img)
+    assert max(l for _, l in s.symbols) >= 15
+
+
 def test_v2_header(gpu, orc):
     _check(gpu, orc, gpu.generate(9, 0.5, 50_001), force_version=2)
 
