@@ -680,6 +680,7 @@ extern "C" int gh_ectx_encode(gh_ectx* e, float* kernel_ms) {
     uint32_t maxlen = 1;
     for (int v = 0; v < 256; ++v) maxlen = std::max<uint32_t>(maxlen, pl.len[v]);
     const uint32_t ew = (1024u + ECHUNK * maxlen + 64u) / 32u + 2u, eg = (1024u + ECHUNK * maxlen) / 1024u + 2u;
+    if (ew > (uint32_t)EWORDS || eg > (uint32_t)EGAPW) return fail(GH_E_TABLE, "code longer than 16 bits");
     const size_t dyn = 4ull * (ew + eg);
     int pb = 0, pw = 0;  // persistent grids: what is resident at once
     GH_EHIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pb, (const void*)gh_enc_bits_kernel, ETB, 0));
